@@ -1,0 +1,187 @@
+/*
+ * tlod.h — C ABI of the MI355X-native (gfx950) hot path for the domain-adaptive
+ * Faster R-CNN training step of Transfer-Learning-Library-for-Object-Detection.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + sizes; no framework types cross this boundary;
+ *   - every call is stream-ordered and asynchronous on `stream` (a hipStream_t; NULL =
+ *     the legacy default stream).  No entry point allocates, frees or synchronises, so a
+ *     caller may capture any of them into a hipGraph;
+ *   - scratch is caller-provided (`ws`, `ws_bytes`); query sizes with *_workspace_bytes;
+ *   - return 0 on success, a negative tlod_status on failure with a message available
+ *     from tlod_last_error() (thread-local).  Nothing ever calls exit() (the reference's
+ *     launchers do: roi_align_kernel.cu:84-88);
+ *   - tensors are contiguous NCHW float32 (the reference's layout and dtype).
+ *
+ * Each entry point names the reference interface it replaces (paths relative to the
+ * reference checkout).
+ */
+#ifndef TLOD_H_
+#define TLOD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* tlod_stream_t; /* hipStream_t */
+
+enum tlod_status {
+  TLOD_OK = 0,
+  TLOD_EINVAL = -1,
+  TLOD_EHIP = -2,
+  TLOD_EWORKSPACE = -3,
+  TLOD_EUNSUPPORTED = -4
+};
+
+int tlod_abi_version(void);
+const char* tlod_last_error(void);
+
+/* ------------------------------------------------------------------ NMS
+ * Replaces: nms_cuda(THCudaIntTensor* keep_out, THCudaTensor* boxes, THCudaIntTensor*
+ *   num_out, float thresh)            lib/model/nms/src/nms_cuda.c:8-19
+ *   -> nms_cuda_compute(...)          lib/model/nms/src/nms_cuda_kernel.cu:87-161
+ * dets: n x dim (dim >= 4: x1,y1,x2,y2[,score]) already sorted by score, descending.
+ * keep: int32[n] indices into dets (only the first *num_keep are written);
+ * num_keep: one int32 on device.  max_keep > 0 stops after that many survivors (the
+ * caller's keep[:post_nms_topN], proposal_layer.py:151-152); <= 0 keeps all.
+ * IoU semantics of devIoU (nms_cuda_kernel.cu:31-39): "+1" areas, suppress if IoU > thresh.
+ * Everything (mask and the greedy scan) runs on the device: no host round trip. */
+size_t tlod_nms_workspace_bytes(int n);
+int tlod_nms_f32(const float* dets, int n, int dim, float thresh, int max_keep,
+                 int32_t* keep, int32_t* num_keep, void* ws, size_t ws_bytes,
+                 tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ RoIAlign
+ * Replaces: roi_align_forward_cuda / roi_align_backward_cuda
+ *   lib/model/roi_align/src/roi_align_cuda.c:7-76 (kernels roi_align_kernel.cu:15-143).
+ * feat (B,C,H,W), rois (R,5) = (batch, x1, y1, x2, y2) in image coords.
+ * fwd writes out (R,C,ah,aw) (no pre-zeroing needed).  bwd ACCUMULATES into
+ * bottom_grad (B,C,H,W): zero it first (the reference's caller does, roi_align.py:42).
+ * The *_avg variants fuse RoIAlignAvg (modules/roi_align.py:18-29): align at
+ * (ph+1)x(pw+1) then avg_pool2d(2, stride 1) -> (R,C,ph,pw), forward and backward. */
+int tlod_roi_align_fwd_f32(const float* feat, int B, int C, int H, int W,
+                           const float* rois, int R, int ah, int aw, float scale,
+                           float* out, tlod_stream_t stream);
+int tlod_roi_align_bwd_f32(const float* top_grad, int B, int C, int H, int W,
+                           const float* rois, int R, int ah, int aw, float scale,
+                           float* bottom_grad, tlod_stream_t stream);
+int tlod_roi_align_avg_fwd_f32(const float* feat, int B, int C, int H, int W,
+                               const float* rois, int R, int ph, int pw, float scale,
+                               float* out, tlod_stream_t stream);
+int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W,
+                               const float* rois, int R, int ph, int pw, float scale,
+                               float* bottom_grad, tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ RoIPool
+ * Replaces: roi_pooling_forward_cuda / roi_pooling_backward_cuda
+ *   lib/model/roi_pooling/src/roi_pooling_cuda.c (kernels roi_pooling_kernel.cu:24-203).
+ * argmax: int32 (R,C,ph,pw), flat index into feat or -1 for an empty bin.
+ * bwd ACCUMULATES into bottom_grad (zero it first); it scatters through argmax
+ * (equal sums to the reference's O(B*C*H*W*R) gather). */
+int tlod_roi_pool_fwd_f32(const float* feat, int B, int C, int H, int W,
+                          const float* rois, int R, int ph, int pw, float scale,
+                          float* out, int32_t* argmax, tlod_stream_t stream);
+int tlod_roi_pool_bwd_f32(const float* top_grad, const int32_t* argmax, int R, int C,
+                          int ph, int pw, float* bottom_grad, tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ Proposal layer
+ * Replaces: _ProposalLayer.forward   lib/model/rpn/proposal_layer.py:49-161
+ * cls_prob (B,2A,H,W) (fg = channels A..2A-1), bbox_deltas (B,4A,H,W), im_info (B,3),
+ * base_anchors (A,4) [generate_anchors order].  rois_out (B,post_nms,5), zero padded,
+ * column 0 = batch index.  Decode+clip, stable descending sort, top pre_nms, NMS,
+ * top post_nms — all on device.  `props_out` (optional, may be NULL) receives the
+ * decoded+clipped boxes (B, H*W*A, 4) in anchor order. */
+size_t tlod_proposal_workspace_bytes(int B, int A, int H, int W, int pre_nms);
+int tlod_proposal_f32(const float* cls_prob, const float* bbox_deltas, const float* im_info,
+                      const float* base_anchors, int B, int A, int H, int W,
+                      int feat_stride, int pre_nms, int post_nms, float nms_thresh,
+                      float* rois_out, float* props_out, void* ws, size_t ws_bytes,
+                      tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ Anchor target
+ * Replaces: _AnchorTargetLayer.forward   lib/model/rpn/anchor_target_layer.py:48-193
+ * Two phases so the reference's host-RNG draws can be replayed exactly:
+ *   1. tlod_anchor_target_label_f32: inside filter (image 0's size, :83-87), IoU with
+ *      the reference's masks, max/argmax, gt-max ties, thresholds -> pre-sampling
+ *      labels; writes counts[B*2] = (#fg, #bg) per image (device int32).
+ *   2. tlod_anchor_target_sample_f32: fg/bg subsampling, targets, weights, unmap and
+ *      the output layouts labels (B,1,A*H,W), targets/inside_w/outside_w (B,4A,H,W).
+ *      Permutations: if `perm` is non-NULL it holds the np.random.permutation draws in
+ *      the reference's call order (:131 then :143, image by image), concatenated;
+ *      perm_off[2*B+1] (device int32 prefix offsets) delimits them: image b's fg draw is
+ *      perm[perm_off[2b] .. perm_off[2b+1]), its bg draw perm[perm_off[2b+1] ..
+ *      perm_off[2b+2]) (empty when that image did not subsample).  If `perm` is NULL a
+ *      counter-based device RNG keyed by `seed` draws the same distribution.
+ * tlod_anchor_target_f32 = both phases with the device RNG (no host sync).
+ * gt_boxes (B,G,5), im_info (B,3). */
+typedef struct tlod_rpn_cfg {
+  float pos_overlap;   /* 0.7 RPN_POSITIVE_OVERLAP */
+  float neg_overlap;   /* 0.3 RPN_NEGATIVE_OVERLAP */
+  float fg_fraction;   /* 0.5 RPN_FG_FRACTION */
+  int batch_size;      /* 256 RPN_BATCHSIZE */
+  int clobber_positives; /* 0 */
+  float inside_weight; /* 1.0 RPN_BBOX_INSIDE_WEIGHTS[0] */
+  int allowed_border;  /* 0 */
+} tlod_rpn_cfg;
+
+size_t tlod_anchor_target_workspace_bytes(int B, int A, int H, int W, int G);
+int tlod_anchor_target_label_f32(const float* base_anchors, int A, int H, int W, int feat_stride,
+                                 const float* gt_boxes, int B, int G, const float* im_info,
+                                 const tlod_rpn_cfg* cfg, int32_t* counts, void* ws,
+                                 size_t ws_bytes, tlod_stream_t stream);
+int tlod_anchor_target_sample_f32(const float* base_anchors, int A, int H, int W, int feat_stride,
+                                  const float* gt_boxes, int B, int G, const tlod_rpn_cfg* cfg,
+                                  const int32_t* perm, const int32_t* perm_off, uint64_t seed,
+                                  float* labels, float* bbox_targets, float* inside_w,
+                                  float* outside_w, void* ws, size_t ws_bytes,
+                                  tlod_stream_t stream);
+int tlod_anchor_target_f32(const float* base_anchors, int A, int H, int W, int feat_stride,
+                           const float* gt_boxes, int B, int G, const float* im_info,
+                           const tlod_rpn_cfg* cfg, uint64_t seed, int32_t* counts,
+                           float* labels, float* bbox_targets, float* inside_w,
+                           float* outside_w, void* ws, size_t ws_bytes, tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ Proposal target
+ * Replaces: _ProposalTargetLayer.forward  lib/model/rpn/proposal_target_layer_cascade.py:33-212
+ * rois (B,R,5) + gt (B,G,5) appended (:39-43) -> S sampled RoIs per image.
+ * Phase 1 writes counts[B*2] = (#fg, #bg candidates).  Phase 2 samples: explicit mode
+ * takes, per image, the np.random.permutation(#fg) draw (fg_perm, concatenated, offsets
+ * perm_off[B+1]) and the np.random.rand(k) draw as float64 (rand, concatenated,
+ * offsets rand_off[B+1]); NULL -> device RNG keyed by `seed`.
+ * Outputs rois_out (B,S,5), labels (B,S), targets (B,S,4) normalised by means/stds,
+ * inside_w, outside_w (B,S,4). */
+typedef struct tlod_rcnn_cfg {
+  int batch_size;      /* 256 TRAIN.BATCH_SIZE (cfgs/vgg16.yml) */
+  float fg_fraction;   /* 0.25 */
+  float fg_thresh;     /* 0.5 */
+  float bg_thresh_hi;  /* 0.5 */
+  float bg_thresh_lo;  /* 0.0 (cfgs/vgg16.yml) */
+  float means[4];      /* 0,0,0,0 */
+  float stds[4];       /* .1,.1,.2,.2 */
+  float inside_weight[4]; /* 1,1,1,1 */
+} tlod_rcnn_cfg;
+
+size_t tlod_proposal_target_workspace_bytes(int B, int R, int G);
+int tlod_proposal_target_count_f32(const float* rois, int B, int R, const float* gt_boxes,
+                                   int G, const tlod_rcnn_cfg* cfg, int32_t* counts,
+                                   void* ws, size_t ws_bytes, tlod_stream_t stream);
+int tlod_proposal_target_sample_f32(const float* rois, int B, int R, const float* gt_boxes,
+                                    int G, const tlod_rcnn_cfg* cfg, const int32_t* fg_perm,
+                                    const int32_t* perm_off, const double* rand,
+                                    const int32_t* rand_off, uint64_t seed,
+                                    float* rois_out, float* labels, float* targets,
+                                    float* inside_w, float* outside_w, void* ws,
+                                    size_t ws_bytes, tlod_stream_t stream);
+int tlod_proposal_target_f32(const float* rois, int B, int R, const float* gt_boxes, int G,
+                             const tlod_rcnn_cfg* cfg, uint64_t seed, int32_t* counts,
+                             float* rois_out, float* labels, float* targets,
+                             float* inside_w, float* outside_w, void* ws, size_t ws_bytes,
+                             tlod_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TLOD_H_ */

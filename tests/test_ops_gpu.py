@@ -1,0 +1,123 @@
+"""Parity of the HIP NMS / RoIAlign / RoIPool kernels with the CPU oracle (C ABI path).
+
+Bars: NMS keep indices and RoIPool argmax bit-exact; RoIAlign / RoIPool forward values
+bit-exact (the kernels restate the CUDA arithmetic with -ffp-contract=off); backward
+values (atomic accumulation, order-dependent) within rtol 1e-5 / atol 1e-6.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import clustered_boxes, random_boxes, sorted_dets
+from oracle import nms as onms
+from oracle import roi as oroi
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _nms(d, thr, max_keep=0):
+    from tlod.nms import nms
+    k = nms(torch.from_numpy(d).to(dev), thr, max_keep=max_keep)
+    return np.asarray([]) if isinstance(k, list) else k.cpu().numpy()
+
+
+@pytest.mark.parametrize("n,thr,kind", [(12000, 0.7, "clustered"), (12000, 0.7, "random"),
+                                        (6000, 0.7, "clustered"), (300, 0.3, "clustered"),
+                                        (65, 0.5, "clustered"), (64, 0.5, "clustered"),
+                                        (1, 0.7, "random"), (2000, 0.0, "random"),
+                                        (3000, 1.0, "clustered")])
+def test_nms_bit_exact(n, thr, kind):
+    rng = np.random.default_rng(n + int(thr * 10))
+    boxes = clustered_boxes(rng, n) if kind == "clustered" else random_boxes(rng, n)
+    d = sorted_dets(boxes, rng)
+    ref = onms.nms(d, thr)
+    got = _nms(d, thr)
+    assert got.dtype == np.int32
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_nms_max_keep_and_duplicates():
+    rng = np.random.default_rng(7)
+    b = clustered_boxes(rng, 5000, clusters=400)
+    b[100:200] = b[100]  # exact duplicates: IoU == 1
+    d = sorted_dets(b, rng)
+    for mk in (1, 63, 64, 65, 300, 2000):
+        np.testing.assert_array_equal(_nms(d, 0.7, mk), onms.nms(d, 0.7, max_keep=mk))
+
+
+def test_nms_empty():
+    from tlod.nms import nms
+    assert nms(torch.zeros((0, 5), device=dev), 0.7) == []
+
+
+def _feat(rng, B=1, C=64, H=37, W=62):
+    return rng.standard_normal((B, C, H, W)).astype(np.float32)
+
+
+def _rois(rng, R, B=1, W=1000, H=600, edge=True):
+    b = random_boxes(rng, R, W, H, 4, 500)
+    if edge:  # malformed / out-of-image / tiny boxes
+        b[0] = [W - 2, H - 2, W + 40, H + 40]
+        b[1] = [-30, -30, 5, 5]
+        b[2] = [100, 100, 90, 95]   # x2 < x1
+        b[3] = [0, 0, 0, 0]
+        b[4] = [10.5, 20.25, 10.5, 20.25]
+    bi = rng.integers(0, B, R).astype(np.float32)
+    return np.concatenate([bi[:, None], b], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("B,C,H,W,R,ah,aw", [(1, 64, 37, 62, 128, 8, 8), (2, 32, 20, 30, 50, 8, 8),
+                                             (1, 16, 9, 11, 40, 4, 6)])
+def test_roi_align_fwd_bwd(B, C, H, W, R, ah, aw):
+    from tlod.roi_align import RoIAlignFunction
+    rng = np.random.default_rng(B * 100 + C)
+    f = _feat(rng, B, C, H, W)
+    r = _rois(rng, R, B, W * 16, H * 16)
+    ft = torch.from_numpy(f).to(dev).requires_grad_(True)
+    out = RoIAlignFunction.apply(ft, torch.from_numpy(r).to(dev), ah, aw, 1.0 / 16)
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), oroi.roi_align_fwd(f, r, ah, aw, 1.0 / 16))
+    g = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(dev))
+    ref = oroi.roi_align_bwd(g, r, B, C, H, W, 1.0 / 16)
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,C,H,W,R", [(1, 512, 37, 62, 256), (1, 100, 37, 75, 300), (2, 64, 12, 16, 33)])
+def test_roi_align_avg_fused(B, C, H, W, R):
+    from tlod.roi_align import RoIAlignAvg
+    rng = np.random.default_rng(R)
+    f = _feat(rng, B, C, H, W)
+    r = _rois(rng, R, B, W * 16, H * 16)
+    ft = torch.from_numpy(f).to(dev).requires_grad_(True)
+    out = RoIAlignAvg(7, 7, 1.0 / 16)(ft, torch.from_numpy(r).to(dev))
+    assert out.shape == (R, C, 7, 7)
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), oroi.roi_align_avg_fwd(f, r, 7, 7, 1.0 / 16))
+    g = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(dev))
+    ref = oroi.roi_align_avg_bwd(g, r, B, C, H, W, 1.0 / 16)
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,C,H,W,R", [(1, 64, 37, 62, 128), (2, 16, 20, 25, 40)])
+def test_roi_pool_fwd_bwd(B, C, H, W, R):
+    from tlod.roi_pool import roi_pool_with_argmax
+    rng = np.random.default_rng(R + C)
+    f = _feat(rng, B, C, H, W)
+    r = _rois(rng, R, B, W * 16, H * 16)
+    ft = torch.from_numpy(f).to(dev).requires_grad_(True)
+    out, arg = roi_pool_with_argmax(ft, torch.from_numpy(r).to(dev), 7, 7, 1.0 / 16)
+    ro, ra = oroi.roi_pool_fwd(f, r, 7, 7, 1.0 / 16)
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), ro)
+    np.testing.assert_array_equal(arg.cpu().numpy(), ra)
+    g = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(dev))
+    ref = oroi.roi_pool_bwd(g, ra, r, B, C, H, W, 1.0 / 16)
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_roi_ops_empty_rois():
+    from tlod.roi_align import RoIAlignAvg
+    f = torch.randn(1, 8, 10, 10, device=dev)
+    out = RoIAlignAvg(7, 7, 1.0 / 16)(f, torch.zeros((0, 5), device=dev))
+    assert out.shape == (0, 8, 7, 7)

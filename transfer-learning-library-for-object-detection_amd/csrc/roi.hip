@@ -1,0 +1,309 @@
+// RoIAlign / RoIAlignAvg / RoIPool forward + backward for gfx950.
+//
+// Numerics follow the reference CUDA kernels literally (compiled here with
+// -ffp-contract=off): lib/model/roi_align/src/roi_align_kernel.cu:15-143 — note the
+// ``1.`` double literals, reproduced as double arithmetic — and
+// lib/model/roi_pooling/src/roi_pooling_kernel.cu:24-93.
+//
+// Layout choices (MI355X-first, not a translation of the reference launch shape):
+//   * RoIAlignAvg is fused: one workgroup per (roi, 64 channels) samples the
+//     (ph+1)x(pw+1) grid into LDS and writes the 2x2/s1-averaged (ph,pw) output as one
+//     contiguous, coalesced slab (the reference writes the 8x8 map to HBM, then a
+//     second torch kernel re-reads it).  Backward fuses avg_pool2d's backward.
+//   * RoIPool backward scatters through argmax (O(R*C*ph*pw) atomics) instead of the
+//     reference's O(B*C*H*W*R) gather (roi_pooling_kernel.cu:128-203).
+#include <algorithm>
+#include <cfloat>
+
+#include "common.h"
+#include "tlod.h"
+
+namespace tlod {
+
+// roi_align_kernel.cu:30-53 for one sample (ph, pw) of roi r.
+__device__ __forceinline__ void align_axis(float start, float end, int n_samples, int p,
+                                           int limit, int* idx, float* ratio, bool* valid) {
+  float len = fmaxf((float)((double)(end - start) + 1.), 0.f);
+  float bin = (float)((double)len / ((double)n_samples - 1.));
+  float v = (float)p * bin + start;
+  int s = (int)fminf((float)floor((double)v), (float)(limit - 2));
+  *idx = s;
+  *ratio = v - (float)s;
+  *valid = !(v < 0.f || v >= (float)limit);
+}
+
+__device__ __forceinline__ float align_sample(const float* __restrict__ plane, int W, int y,
+                                              int x, float hr, float wr) {
+  const float ul = plane[y * W + x], ur = plane[y * W + x + 1];
+  const float dl = plane[(y + 1) * W + x], dr = plane[(y + 1) * W + x + 1];
+  // bottom[ul]*(1.-h)*(1.-w) + bottom[ur]*(1.-h)*w + bottom[dl]*h*(1.-w) + bottom[dr]*h*w
+  double t1 = ((double)ul * (1. - (double)hr)) * (1. - (double)wr);
+  double t2 = ((double)ur * (1. - (double)hr)) * (double)wr;
+  double t3 = (double)(dl * hr) * (1. - (double)wr);
+  double t4 = (double)((dr * hr) * wr);
+  return (float)(((t1 + t2) + t3) + t4);
+}
+
+// ------------------------------------------------------------ plain RoIAlign
+__global__ void roi_align_fwd_kernel(int total, const float* __restrict__ feat, float scale,
+                                     int C, int H, int W, int ah, int aw,
+                                     const float* __restrict__ rois, float* __restrict__ out) {
+  for (int index = blockIdx.x * blockDim.x + threadIdx.x; index < total;
+       index += blockDim.x * gridDim.x) {
+    const int pw = index % aw;
+    const int ph = (index / aw) % ah;
+    const int c = (index / aw / ah) % C;
+    const int n = index / aw / ah / C;
+    const float* r = rois + n * 5;
+    const int b = (int)r[0];
+    int y, x;
+    float hr, wr;
+    bool vy, vx;
+    align_axis(r[2] * scale, r[4] * scale, ah, ph, H, &y, &hr, &vy);
+    align_axis(r[1] * scale, r[3] * scale, aw, pw, W, &x, &wr, &vx);
+    out[index] = (vy && vx)
+                     ? align_sample(feat + ((size_t)b * C + c) * H * W, W, y, x, hr, wr)
+                     : 0.f;
+  }
+}
+
+__device__ __forceinline__ void align_scatter(float* __restrict__ plane, int W, int y, int x,
+                                              float hr, float wr, float td) {
+  // roi_align_kernel.cu:137-140 — atomicAdd arguments rounded to float as in the source.
+  const float om = 1.f - wr;  // (1 - w_ratio) is float
+  atomicAdd(plane + y * W + x, (float)(((double)td * (1. - (double)hr)) * (double)om));
+  atomicAdd(plane + y * W + x + 1, (float)(((double)td * (1. - (double)hr)) * (double)wr));
+  atomicAdd(plane + (y + 1) * W + x, (td * hr) * om);
+  atomicAdd(plane + (y + 1) * W + x + 1, (td * hr) * wr);
+}
+
+__global__ void roi_align_bwd_kernel(int total, const float* __restrict__ top, float scale,
+                                     int C, int H, int W, int ah, int aw,
+                                     const float* __restrict__ rois, float* __restrict__ grad) {
+  for (int index = blockIdx.x * blockDim.x + threadIdx.x; index < total;
+       index += blockDim.x * gridDim.x) {
+    const int pw = index % aw;
+    const int ph = (index / aw) % ah;
+    const int c = (index / aw / ah) % C;
+    const int n = index / aw / ah / C;
+    const float* r = rois + n * 5;
+    const int b = (int)r[0];
+    int y, x;
+    float hr, wr;
+    bool vy, vx;
+    align_axis(r[2] * scale, r[4] * scale, ah, ph, H, &y, &hr, &vy);
+    align_axis(r[1] * scale, r[3] * scale, aw, pw, W, &x, &wr, &vx);
+    if (vy && vx) align_scatter(grad + ((size_t)b * C + c) * H * W, W, y, x, hr, wr, top[index]);
+  }
+}
+
+// ------------------------------------------------------------ fused RoIAlignAvg
+constexpr int kAvgCh = 64;     // channels per workgroup
+constexpr int kAvgThreads = 256;
+
+// grid (ceil(C/64), R).  S = (ph+1)*(pw+1) <= 64 samples per channel.
+__global__ void __launch_bounds__(kAvgThreads) roi_align_avg_fwd_kernel(
+    const float* __restrict__ feat, float scale, int C, int H, int W, int ph, int pw,
+    const float* __restrict__ rois, float* __restrict__ out) {
+  const int ah = ph + 1, aw = pw + 1, S = ah * aw;
+  const int r = blockIdx.y, c0 = blockIdx.x * kAvgCh;
+  const int nc = min(kAvgCh, C - c0);
+  __shared__ int gy[8], gx[8];
+  __shared__ float ghr[8], gwr[8];
+  __shared__ bool gvy[8], gvx[8];
+  __shared__ float samp[kAvgCh * 65];
+  const float* ro = rois + r * 5;
+  const int t = threadIdx.x;
+  if (t < ah) align_axis(ro[2] * scale, ro[4] * scale, ah, t, H, &gy[t], &ghr[t], &gvy[t]);
+  if (t >= 32 && t < 32 + aw) {
+    const int p = t - 32;
+    align_axis(ro[1] * scale, ro[3] * scale, aw, p, W, &gx[p], &gwr[p], &gvx[p]);
+  }
+  __syncthreads();
+  const int b = (int)ro[0];
+  const float* base = feat + ((size_t)b * C + c0) * H * W;
+  for (int e = t; e < nc * S; e += kAvgThreads) {
+    const int c = e / S, s = e % S;
+    const int sy = s / aw, sx = s % aw;
+    float v = 0.f;
+    if (gvy[sy] && gvx[sx])
+      v = align_sample(base + (size_t)c * H * W, W, gy[sy], gx[sx], ghr[sy], gwr[sx]);
+    samp[c * 65 + s] = v;
+  }
+  __syncthreads();
+  // avg_pool2d(2, s1): ((((0+a)+b)+c)+d)/4 in float, rows then columns.
+  const int P = ph * pw;
+  float* o = out + ((size_t)r * C + c0) * P;
+  for (int e = t; e < nc * P; e += kAvgThreads) {
+    const int c = e / P, q = e % P;
+    const int oy = q / pw, ox = q % pw;
+    const float* sp = samp + c * 65 + oy * aw + ox;
+    float acc = 0.f;
+    acc += sp[0];
+    acc += sp[1];
+    acc += sp[aw];
+    acc += sp[aw + 1];
+    o[e] = acc / 4.f;
+  }
+}
+
+__global__ void __launch_bounds__(kAvgThreads) roi_align_avg_bwd_kernel(
+    const float* __restrict__ top, float scale, int C, int H, int W, int ph, int pw,
+    const float* __restrict__ rois, float* __restrict__ grad) {
+  const int ah = ph + 1, aw = pw + 1, S = ah * aw, P = ph * pw;
+  const int r = blockIdx.y, c0 = blockIdx.x * kAvgCh;
+  const int nc = min(kAvgCh, C - c0);
+  __shared__ int gy[8], gx[8];
+  __shared__ float ghr[8], gwr[8];
+  __shared__ bool gvy[8], gvx[8];
+  __shared__ float g7[kAvgCh * 49 + 64];
+  const float* ro = rois + r * 5;
+  const int t = threadIdx.x;
+  if (t < ah) align_axis(ro[2] * scale, ro[4] * scale, ah, t, H, &gy[t], &ghr[t], &gvy[t]);
+  if (t >= 32 && t < 32 + aw) {
+    const int p = t - 32;
+    align_axis(ro[1] * scale, ro[3] * scale, aw, p, W, &gx[p], &gwr[p], &gvx[p]);
+  }
+  const float* tp = top + ((size_t)r * C + c0) * P;
+  for (int e = t; e < nc * P; e += kAvgThreads) g7[e] = tp[e] / 4.f;  // coalesced slab
+  __syncthreads();
+  const int b = (int)ro[0];
+  float* gbase = grad + ((size_t)b * C + c0) * H * W;
+  for (int e = t; e < nc * S; e += kAvgThreads) {
+    const int c = e / S, s = e % S;
+    const int sy = s / aw, sx = s % aw;
+    if (!(gvy[sy] && gvx[sx])) continue;
+    // avg_pool2d backward: sum over covering windows, py outer, px inner (float).
+    float g = 0.f;
+    const float* gp = g7 + c * P;
+    for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
+      for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
+    align_scatter(gbase + (size_t)c * H * W, W, gy[sy], gx[sx], ghr[sy], gwr[sx], g);
+  }
+}
+
+// ------------------------------------------------------------ RoIPool
+__global__ void roi_pool_fwd_kernel(int total, const float* __restrict__ feat, float scale,
+                                    int C, int H, int W, int PH, int PW,
+                                    const float* __restrict__ rois, float* __restrict__ out,
+                                    int32_t* __restrict__ argmax) {
+  for (int index = blockIdx.x * blockDim.x + threadIdx.x; index < total;
+       index += blockDim.x * gridDim.x) {
+    const int pw = index % PW;
+    const int ph = (index / PW) % PH;
+    const int c = (index / PW / PH) % C;
+    const int n = index / PW / PH / C;
+    const float* r = rois + n * 5;
+    const int b = (int)r[0];
+    const int sw = (int)round(r[1] * scale), sh = (int)round(r[2] * scale);
+    const int ew = (int)round(r[3] * scale), eh = (int)round(r[4] * scale);
+    const int rw = max(ew - sw + 1, 1), rh = max(eh - sh + 1, 1);
+    const float bh = (float)rh / (float)PH, bw = (float)rw / (float)PW;
+    int hs = (int)floorf((float)ph * bh), ws = (int)floorf((float)pw * bw);
+    int he = (int)ceilf((float)(ph + 1) * bh), we = (int)ceilf((float)(pw + 1) * bw);
+    hs = min(max(hs + sh, 0), H);
+    he = min(max(he + sh, 0), H);
+    ws = min(max(ws + sw, 0), W);
+    we = min(max(we + sw, 0), W);
+    const bool empty = (he <= hs) || (we <= ws);
+    float maxval = empty ? 0.f : -FLT_MAX;
+    int maxidx = -1;
+    const size_t off = ((size_t)b * C + c) * H * W;
+    for (int h = hs; h < he; ++h)
+      for (int w = ws; w < we; ++w) {
+        const float v = feat[off + h * W + w];
+        if (v > maxval) { maxval = v; maxidx = (int)(off + h * W + w); }
+      }
+    out[index] = maxval;
+    argmax[index] = maxidx;
+  }
+}
+
+__global__ void roi_pool_bwd_kernel(int total, const float* __restrict__ top,
+                                    const int32_t* __restrict__ argmax,
+                                    float* __restrict__ grad) {
+  for (int index = blockIdx.x * blockDim.x + threadIdx.x; index < total;
+       index += blockDim.x * gridDim.x) {
+    const int a = argmax[index];
+    if (a >= 0) atomicAdd(grad + a, top[index]);
+  }
+}
+
+static inline int grid_for(int total, int block) { return std::min(div_up(total, block), 256 * 32); }
+
+}  // namespace tlod
+
+using namespace tlod;
+
+extern "C" int tlod_roi_align_fwd_f32(const float* feat, int B, int C, int H, int W,
+                                      const float* rois, int R, int ah, int aw, float scale,
+                                      float* out, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0 && ah >= 2 && aw >= 2, "bad shape");
+  const int total = R * C * ah * aw;
+  if (total == 0) return kOk;
+  hipLaunchKernelGGL(roi_align_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, total, feat, scale, C, H, W, ah, aw, rois, out);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_roi_align_bwd_f32(const float* top_grad, int B, int C, int H, int W,
+                                      const float* rois, int R, int ah, int aw, float scale,
+                                      float* bottom_grad, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0 && ah >= 2 && aw >= 2, "bad shape");
+  const int total = R * C * ah * aw;
+  if (total == 0) return kOk;
+  hipLaunchKernelGGL(roi_align_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, total, top_grad, scale, C, H, W, ah, aw, rois,
+                     bottom_grad);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_roi_align_avg_fwd_f32(const float* feat, int B, int C, int H, int W,
+                                          const float* rois, int R, int ph, int pw, float scale,
+                                          float* out, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0, "bad shape");
+  TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
+  if (R == 0) return kOk;
+  hipLaunchKernelGGL(roi_align_avg_fwd_kernel, dim3(div_up(C, kAvgCh), R), dim3(kAvgThreads), 0,
+                     (hipStream_t)stream, feat, scale, C, H, W, ph, pw, rois, out);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W,
+                                          const float* rois, int R, int ph, int pw, float scale,
+                                          float* bottom_grad, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0, "bad shape");
+  TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
+  if (R == 0) return kOk;
+  hipLaunchKernelGGL(roi_align_avg_bwd_kernel, dim3(div_up(C, kAvgCh), R), dim3(kAvgThreads), 0,
+                     (hipStream_t)stream, top_grad, scale, C, H, W, ph, pw, rois, bottom_grad);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_roi_pool_fwd_f32(const float* feat, int B, int C, int H, int W,
+                                     const float* rois, int R, int ph, int pw, float scale,
+                                     float* out, int32_t* argmax, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0 && R >= 0 && ph > 0 && pw > 0, "bad shape");
+  TLOD_CHECK_ARG((size_t)B * C * H * W < (1ull << 31), "feature map too large for int32 argmax");
+  const int total = R * C * ph * pw;
+  if (total == 0) return kOk;
+  hipLaunchKernelGGL(roi_pool_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, total, feat, scale, C, H, W, ph, pw, rois, out, argmax);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_roi_pool_bwd_f32(const float* top_grad, const int32_t* argmax, int R, int C,
+                                     int ph, int pw, float* bottom_grad, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(R >= 0 && C > 0 && ph > 0 && pw > 0, "bad shape");
+  const int total = R * C * ph * pw;
+  if (total == 0) return kOk;
+  hipLaunchKernelGGL(roi_pool_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, total, top_grad, argmax, bottom_grad);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}

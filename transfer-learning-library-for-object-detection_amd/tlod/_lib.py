@@ -1,0 +1,131 @@
+"""ctypes binding of libtlod.so (the C ABI declared in include/tlod.h).
+
+This is the ONLY way the Python host side reaches the MI355X kernels.  There is no CPU
+fallback anywhere in the product path: if the library is missing, or a tensor is not on
+the GPU, calls raise.  (The CPU restatement under ``oracle/`` is test infrastructure and
+is never imported from here.)
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libtlod.so")
+
+c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
+c_size_t, c_void_p, c_uint64 = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64
+P = c_void_p  # every device pointer / stream crosses as void*
+
+
+class RpnCfg(ctypes.Structure):
+    """tlod_rpn_cfg (include/tlod.h)."""
+    _fields_ = [("pos_overlap", c_float), ("neg_overlap", c_float), ("fg_fraction", c_float),
+                ("batch_size", c_int), ("clobber_positives", c_int),
+                ("inside_weight", c_float), ("allowed_border", c_int)]
+
+
+class RcnnCfg(ctypes.Structure):
+    """tlod_rcnn_cfg (include/tlod.h)."""
+    _fields_ = [("batch_size", c_int), ("fg_fraction", c_float), ("fg_thresh", c_float),
+                ("bg_thresh_hi", c_float), ("bg_thresh_lo", c_float),
+                ("means", c_float * 4), ("stds", c_float * 4), ("inside_weight", c_float * 4)]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "tlod_abi_version": (c_int, []),
+    "tlod_last_error": (ctypes.c_char_p, []),
+    "tlod_nms_workspace_bytes": (c_size_t, [c_int]),
+    "tlod_nms_f32": (c_int, [P, c_int, c_int, c_float, c_int, P, P, P, c_size_t, P]),
+    "tlod_roi_align_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
+                                       c_float, P, P]),
+    "tlod_roi_align_bwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
+                                       c_float, P, P]),
+    "tlod_roi_align_avg_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
+                                           c_float, P, P]),
+    "tlod_roi_align_avg_bwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
+                                           c_float, P, P]),
+    "tlod_roi_pool_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
+                                      c_float, P, P, P]),
+    "tlod_roi_pool_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_proposal_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "tlod_proposal_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_float, P, P, P, c_size_t, P]),
+    "tlod_anchor_target_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "tlod_anchor_target_label_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P,
+                                             ctypes.POINTER(RpnCfg), P, P, c_size_t, P]),
+    "tlod_anchor_target_sample_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int,
+                                              ctypes.POINTER(RpnCfg), P, P, c_uint64, P, P, P, P,
+                                              P, c_size_t, P]),
+    "tlod_anchor_target_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P,
+                                       ctypes.POINTER(RpnCfg), c_uint64, P, P, P, P, P, P,
+                                       c_size_t, P]),
+    "tlod_proposal_target_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "tlod_proposal_target_count_f32": (c_int, [P, c_int, c_int, P, c_int, ctypes.POINTER(RcnnCfg),
+                                               P, P, c_size_t, P]),
+    "tlod_proposal_target_sample_f32": (c_int, [P, c_int, c_int, P, c_int, ctypes.POINTER(RcnnCfg),
+                                                P, P, P, P, c_uint64, P, P, P, P, P, P,
+                                                c_size_t, P]),
+    "tlod_proposal_target_f32": (c_int, [P, c_int, c_int, P, c_int, ctypes.POINTER(RcnnCfg),
+                                         c_uint64, P, P, P, P, P, P, P, c_size_t, P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libtlod.so once; raise (never fall back) if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libtlod.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status, what=""):
+    if status != 0:
+        msg = lib().tlod_last_error().decode(errors="replace")
+        raise RuntimeError(f"tlod {what} failed (status {status}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def stream_of(t=None):
+    dev = t.device if t is not None else None
+    return c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def require_cuda(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("tlod ops run on the MI355X only: got a CPU tensor "
+                               "(the reference's CPU kernels are not part of this path)")
+
+
+_ws_cache = {}
+
+
+def workspace(nbytes, device, name):
+    """Grow-only scratch buffer per (op name, device, stream) for the C ABI's
+    caller-provided workspace.  Distinct names keep two-phase ops (anchor target,
+    proposal target) from sharing scratch with ops launched between their phases."""
+    key = (name, str(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
