@@ -181,6 +181,36 @@ int tlod_proposal_target_f32(const float* rois, int B, int R, const float* gt_bo
                              float* inside_w, float* outside_w, void* ws, size_t ws_bytes,
                              tlod_stream_t stream);
 
+
+/* ------------------------------------------------------------------ Convolution
+ * Replaces: the cuDNN fp32 convolutions behind the VGG16 backbone and RPN conv
+ *   (RCNN_base = torchvision vgg16().features[:-1], lib/DAF/vgg16.py:49; RPN_Conv
+ *   lib/model/rpn/rpn.py:28; the DA heads' 1x1 convs lib/DAF/DA.py:40-41).
+ * Stride 1, zero padding KS/2, KS in {1, 3}; NCHW fp32, f32-input MFMA (exact f32 FMAs).
+ * Weight operands are packed once per weight version:
+ *   tlod_conv_pack_fwd_f32  : wk[(ci*KS*KS + s)][co]          = weight[co][ci][s]
+ *   tlod_conv_pack_dgrad_f32: wd[(co*KS*KS + s)][ci]          = weight[co][ci][KS*KS-1-s]
+ * fwd  : y = conv(x, weight) (+ bias) (then ReLU if relu != 0)      y (N,Cout,H,W)
+ * dgrad: dx = conv_transpose(dy, weight)                            dx (N,Cin,H,W)
+ * wgrad: dw (+)= sum_n,p dy (x) x-patches, deterministic split-K    dw (Cout,Cin,KS,KS)
+ *        (accumulate != 0 adds into dw, like autograd grad accumulation)
+ * relu_bwd_bias: g = dy * (y > 0) (y may be NULL: g = dy), db += sum over n,h,w of g
+ *        (db may be NULL).  g may alias dy. */
+int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
+                           tlod_stream_t stream);
+int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, int KS, float* wd,
+                             tlod_stream_t stream);
+int tlod_conv_fwd_f32(const float* x, const float* wk, const float* bias, float* y, int N,
+                      int Cin, int H, int W, int Cout, int KS, int relu, tlod_stream_t stream);
+int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, int N, int Cin, int H,
+                        int W, int Cout, int KS, tlod_stream_t stream);
+size_t tlod_conv_wgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS);
+int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, int accumulate, int N,
+                        int Cin, int H, int W, int Cout, int KS, void* ws, size_t ws_bytes,
+                        tlod_stream_t stream);
+int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db, int N, int C,
+                           int HW, tlod_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

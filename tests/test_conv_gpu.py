@@ -1,0 +1,68 @@
+"""HIP implicit-GEMM convolution (f32 MFMA) vs a plain PyTorch fp64 CPU reference.
+
+Bar (north star: 1e-3 relative for conv activations): we require normwise relative
+error <= 1e-5 and elementwise |err| <= 1e-4 * max|ref| — the f32-input MFMA computes an
+exact f32 FMA chain, so the error is f32 rounding only.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _close(got, ref, tol=1e-5):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    nrm = (got - ref).norm() / max(ref.norm(), 1e-30)
+    assert nrm <= tol, f"normwise rel err {nrm:.3e}"
+    assert (got - ref).abs().max() <= 1e-4 * ref.abs().max() + 1e-30
+
+
+SHAPES = [  # N, Cin, Cout, H, W, KS
+    (2, 64, 128, 37, 75, 3), (1, 3, 64, 50, 70, 3), (2, 256, 256, 30, 40, 3),
+    (1, 512, 512, 37, 62, 3), (1, 32, 64, 5, 7, 3), (1, 130, 132, 9, 33, 3),
+    (2, 512, 512, 20, 31, 1), (1, 512, 24, 37, 62, 1), (1, 512, 48, 11, 13, 1),
+]
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,KS", SHAPES)
+def test_conv_fwd_bwd(N, Cin, Cout, H, W, KS):
+    from tlod.conv import ConvFunction
+    g = torch.Generator().manual_seed(N * 1000 + Cin + Cout + H)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, KS, KS, generator=g) * (2.0 / (Cin * KS * KS)) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    for relu in (False, True):
+        xd, wd, bd = (t.to(dev).requires_grad_(True) for t in (x, w, b))
+        y = ConvFunction.apply(xd, wd, bd, relu)
+        xr, wr, br = (t.double().requires_grad_(True) for t in (x, w, b))
+        yr = F.conv2d(xr, wr, br, padding=KS // 2)
+        if relu:
+            yr = F.relu(yr)
+        _close(y, yr)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy.to(dev))
+        yr.backward(gy.double())
+        _close(xd.grad, xr.grad)
+        _close(wd.grad, wr.grad)
+        _close(bd.grad, br.grad)
+
+
+def test_conv_module_matches_nn_conv2d_keys():
+    from tlod.conv import Conv2d
+    m = Conv2d(64, 128, 3, relu=True)
+    ref = torch.nn.Conv2d(64, 128, 3, padding=1)
+    assert m.state_dict().keys() == ref.state_dict().keys()
+    assert m.weight.shape == ref.weight.shape
+
+
+def test_wgrad_deterministic():
+    from tlod.conv import conv_wgrad
+    g = torch.randn(2, 256, 40, 60, device=dev)
+    x = torch.randn(2, 128, 40, 60, device=dev)
+    a = conv_wgrad(g, x, 3)
+    b = conv_wgrad(g, x, 3)
+    assert torch.equal(a, b)

@@ -1,0 +1,577 @@
+// Implicit-GEMM convolution (stride 1, "same" padding, KSxKS) on gfx950 MFMA, fp32.
+//
+// Replaces the cuDNN convolutions behind the VGG16 backbone and RPN conv
+// (RCNN_base = torchvision vgg16().features[:-1], lib/DAF/vgg16.py:49; RPN_Conv
+// lib/model/rpn/rpn.py:28).  The reference computes in fp32; so do we, on the f32-input
+// MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, one rounding per accumulate), whose
+// dense peak (157.3 TF) is the roofline these kernels are measured against.
+//
+//   fwd  : Y[n,co,p]  = sum_{ci,kh,kw} Wk[(ci,kh,kw)][co] * X[n,ci,p+(kh,kw)-pad]   (+bias, relu)
+//   dgrad: the same kernel with X := dY and Wk := packed flipped/transposed weights
+//   wgrad: dW[co][(ci,kh,kw)] = sum_{n,p} dY[n,co,p] * X[n,ci,p+(kh,kw)-pad]   (split-K slabs)
+//
+// Tiling (CDNA4-first): 256-thread workgroups of 4 wave64s; each wave owns MIx NJ
+// 32x32 accumulator tiles (16 f32 regs each).  The input halo patch of CK channels is
+// staged once in LDS and the KS*KS shifted views are read from it (9x less L2 traffic
+// than an explicit im2col); operand tiles are double-buffered in LDS with the next
+// chunk's global loads held in registers across the MFMA phase (issue early / write
+// late).  Block ids are remapped so each XCD walks a contiguous run of tiles (its L2
+// keeps the shared input patches).
+#include "common.h"
+#include "tlod.h"
+
+namespace tlod {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// XCD-aware bijective remap: consecutive hardware ids round-robin over 8 XCDs; give
+// each XCD a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// ======================================================================= forward
+// Block tile: BM = WM*MI*32 output channels x BN = TH*32 pixels (TH = WN*NJ rows of 32).
+template <int WM, int WN, int MI, int NJ, int CK, int KS>
+struct FwdCfg {
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * MI * 32;
+  static constexpr int TH = WN * NJ;
+  static constexpr int TW = 32;
+  static constexpr int PH = TH + KS - 1, PW = TW + KS - 1;
+  static constexpr int KK = KS * KS;
+  static constexpr int KC = CK * KK;              // GEMM K per chunk
+  static constexpr int A_ELEMS = KC * BM;         // As[KC][BM]
+  static constexpr int B_ELEMS = CK * PH * PW;    // Bs[CK][PH][PW]
+  static constexpr int A_V4 = A_ELEMS / 4;
+  static constexpr int A_PER = (A_V4 + NT - 1) / NT;
+  static constexpr int B_PER = (B_ELEMS + NT - 1) / NT;
+  static constexpr int LDS_FLOATS = 2 * (A_ELEMS + B_ELEMS);
+};
+
+template <int WM, int WN, int MI, int NJ, int CK, int KS>
+__global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
+    const float* __restrict__ X, const float* __restrict__ Wk, const float* __restrict__ bias,
+    float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int relu, int tiles_m,
+    int tiles_w, int tiles_h) {
+  using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* As0 = lds;
+  float* Bs0 = lds + C::A_ELEMS;
+  float* As1 = lds + C::A_ELEMS + C::B_ELEMS;
+  float* Bs1 = As1 + C::A_ELEMS;
+
+  const int nwg = tiles_m * tiles_w * tiles_h * N;
+  int t = xcd_remap(blockIdx.x, nwg);
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int tw = t % tiles_w; t /= tiles_w;
+  const int th = t % tiles_h;
+  const int n = t / tiles_h;
+  const int m0 = mt * C::BM, w0 = tw * C::TW, h0 = th * C::TH;
+  const int pad = KS / 2;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l32 = lane & 31, khalf = lane >> 5;
+
+  const float* Xn = X + (size_t)n * Cin * H * W;
+  const int nchunks = (Cin + CK - 1) / CK;
+  const int Ktot = Cin * C::KK;
+
+  float4 ra[C::A_PER];
+  float rb[C::B_PER];
+
+  auto load_chunk = [&](int ch) {
+    const int k0 = ch * C::KC;
+#pragma unroll
+    for (int i = 0; i < C::A_PER; ++i) {
+      const int e = tid + i * C::NT;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::A_V4) {
+        const int kk = e / (C::BM / 4), mm = (e % (C::BM / 4)) * 4;
+        const int k = k0 + kk, m = m0 + mm;
+        if (k < Ktot && m < Cout) v = *reinterpret_cast<const float4*>(Wk + (size_t)k * Cout + m);
+      }
+      ra[i] = v;
+    }
+    const int ci0 = ch * CK;
+#pragma unroll
+    for (int i = 0; i < C::B_PER; ++i) {
+      const int e = tid + i * C::NT;
+      float v = 0.f;
+      if (e < C::B_ELEMS) {
+        const int ci = e / (C::PH * C::PW), r = (e / C::PW) % C::PH, c = e % C::PW;
+        const int gh = h0 - pad + r, gw = w0 - pad + c, gc = ci0 + ci;
+        if (gc < Cin && gh >= 0 && gh < H && gw >= 0 && gw < W)
+          v = Xn[((size_t)gc * H + gh) * W + gw];
+      }
+      rb[i] = v;
+    }
+  };
+  auto store_chunk = [&](float* As, float* Bs) {
+#pragma unroll
+    for (int i = 0; i < C::A_PER; ++i) {
+      const int e = tid + i * C::NT;
+      if (e < C::A_V4) reinterpret_cast<float4*>(As)[e] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_PER; ++i) {
+      const int e = tid + i * C::NT;
+      if (e < C::B_ELEMS) Bs[e] = rb[i];
+    }
+  };
+
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_chunk(0);
+  store_chunk(As0, Bs0);
+  __syncthreads();
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    float* As = (ch & 1) ? As1 : As0;
+    float* Bs = (ch & 1) ? Bs1 : Bs0;
+    const bool more = ch + 1 < nchunks;
+    if (more) load_chunk(ch + 1);
+    const int kvalid = min(C::KC, (Cin - ch * CK) * C::KK);
+    for (int kk = 0; kk < kvalid; kk += 2) {
+      const int k = kk + khalf;
+      const int ci = k / C::KK, s = k % C::KK;
+      const int kh = s / KS, kw = s % KS;
+      float a[MI], b[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = As[k * C::BM + wm * MI * 32 + i * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[j] = Bs[(ci * C::PH + wn * NJ + j + kh) * C::PW + l32 + kw];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+    if (more) store_chunk((ch & 1) ? As0 : As1, (ch & 1) ? Bs0 : Bs1);
+    __syncthreads();
+  }
+
+  // epilogue: lane owns pixel column l32; rows (co) = (r&3) + 8*(r>>2) + 4*khalf
+  float* Yn = Y + (size_t)n * Cout * H * W;
+  const int w = w0 + l32;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int h = h0 + wn * NJ + j;
+      if (h >= H || w >= W) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        if (co < Cout) {
+          float v = acc[i][j][r];
+          if (bias) v += bias[co];
+          if (relu) v = fmaxf(v, 0.f);
+          Yn[((size_t)co * H + h) * W + w] = v;
+        }
+      }
+    }
+}
+
+// ======================================================================= wgrad
+// Block tile: BM = WM*MI*32 output channels x BN = WN*NJ*32 GEMM columns n=(ci,kh,kw);
+// K = pixels, chunked as TH=2 rows x 32 columns; grid.y = split-K slices.
+template <int WM, int WN, int MI, int NJ, int KS>
+struct WgCfg {
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * MI * 32;
+  static constexpr int BN = WN * NJ * 32;
+  static constexpr int KK = KS * KS;
+  static constexpr int TH = 2, TW = 32, P = TH * TW;  // 64 pixels per chunk
+  static constexpr int PH = TH + KS - 1, PW = TW + KS - 1;
+  static constexpr int NCI = BN / KK + 2;           // channels a column tile can span
+  static constexpr int GP = BM + 1;                  // padded pitch of Gs[p][m]
+  static constexpr int G_ELEMS = P * GP;
+  static constexpr int X_ELEMS = NCI * PH * PW + 1;  // +1: a zero slot for dead columns
+  static constexpr int G_PER = (BM * P + NT - 1) / NT;
+  static constexpr int X_PER = (NCI * PH * PW + NT - 1) / NT;
+  static constexpr int LDS_FLOATS = 2 * (G_ELEMS + X_ELEMS);
+};
+
+template <int WM, int WN, int MI, int NJ, int KS>
+__global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
+    const float* __restrict__ G, const float* __restrict__ X, float* __restrict__ slab, int N,
+    int Cin, int H, int W, int Cout, int tiles_m, int tiles_n, int splits, int chunks_per_split) {
+  using C = WgCfg<WM, WN, MI, NJ, KS>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Gs0 = lds;
+  float* Xs0 = lds + C::G_ELEMS;
+  float* Gs1 = Xs0 + C::X_ELEMS;
+  float* Xs1 = Gs1 + C::G_ELEMS;
+
+  const int nwg = tiles_m * tiles_n * splits;
+  int t = xcd_remap(blockIdx.x, nwg);
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int nt = t % tiles_n;
+  const int split = t / tiles_n;
+  const int m0 = mt * C::BM, n0 = nt * C::BN;
+  const int Ktot = Cin * C::KK;
+  const int cb = n0 / C::KK;
+  const int pad = KS / 2;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l32 = lane & 31, khalf = lane >> 5;
+
+  const int cw = (W + C::TW - 1) / C::TW, chh = (H + C::TH - 1) / C::TH;
+  const int total_chunks = N * chh * cw;
+  const int c_begin = split * chunks_per_split;
+  const int c_end = min(total_chunks, c_begin + chunks_per_split);
+
+  // per-lane B column offsets into Xs (dead columns read the zero slot)
+  int boff[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = n0 + wn * NJ * 32 + j * 32 + l32;
+    if (col < Ktot) {
+      const int ci = col / C::KK - cb, s = col % C::KK;
+      boff[j] = (ci * C::PH + s / KS) * C::PW + s % KS;
+    } else {
+      boff[j] = -1;
+    }
+  }
+
+  float rg[C::G_PER];
+  float rx[C::X_PER];
+  auto load_chunk = [&](int c) {
+    const int cwi = c % cw, r = c / cw;
+    const int chi = r % chh, n = r / chh;
+    const int h0 = chi * C::TH, w0 = cwi * C::TW;
+    const float* Gn = G + (size_t)n * Cout * H * W;
+    const float* Xn = X + (size_t)n * Cin * H * W;
+#pragma unroll
+    for (int i = 0; i < C::G_PER; ++i) {
+      const int e = tid + i * C::NT;  // e -> (m, p), p fastest: 128-B row segments
+      float v = 0.f;
+      if (e < C::BM * C::P) {
+        const int m = e / C::P, p = e % C::P;
+        const int h = h0 + p / C::TW, w = w0 + p % C::TW;
+        if (m0 + m < Cout && h < H && w < W) v = Gn[((size_t)(m0 + m) * H + h) * W + w];
+      }
+      rg[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < C::X_PER; ++i) {
+      const int e = tid + i * C::NT;
+      float v = 0.f;
+      if (e < C::NCI * C::PH * C::PW) {
+        const int ci = e / (C::PH * C::PW), rr = (e / C::PW) % C::PH, cc = e % C::PW;
+        const int gc = cb + ci, gh = h0 - pad + rr, gw = w0 - pad + cc;
+        if (gc < Cin && gh >= 0 && gh < H && gw >= 0 && gw < W)
+          v = Xn[((size_t)gc * H + gh) * W + gw];
+      }
+      rx[i] = v;
+    }
+  };
+  auto store_chunk = [&](float* Gs, float* Xs) {
+#pragma unroll
+    for (int i = 0; i < C::G_PER; ++i) {
+      const int e = tid + i * C::NT;
+      if (e < C::BM * C::P) {
+        const int m = e / C::P, p = e % C::P;
+        Gs[p * C::GP + m] = rg[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < C::X_PER; ++i) {
+      const int e = tid + i * C::NT;
+      if (e < C::NCI * C::PH * C::PW) Xs[e] = rx[i];
+    }
+  };
+
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (tid == 0) { Xs0[C::X_ELEMS - 1] = 0.f; Xs1[C::X_ELEMS - 1] = 0.f; }
+  int zslot[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) zslot[j] = boff[j] < 0;
+
+  if (c_begin < c_end) {
+    load_chunk(c_begin);
+    store_chunk(Gs0, Xs0);
+  }
+  __syncthreads();
+  for (int c = c_begin; c < c_end; ++c) {
+    const int it = c - c_begin;
+    float* Gs = (it & 1) ? Gs1 : Gs0;
+    float* Xs = (it & 1) ? Xs1 : Xs0;
+    const bool more = c + 1 < c_end;
+    if (more) load_chunk(c + 1);
+#pragma unroll 4
+    for (int ks = 0; ks < C::P / 2; ++ks) {
+      const int p = 2 * ks + khalf;
+      const int pofs = (p / C::TW) * C::PW + (p % C::TW);
+      float a[MI], b[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = Gs[p * C::GP + wm * MI * 32 + i * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[j] = zslot[j] ? Xs[C::X_ELEMS - 1] : Xs[boff[j] + pofs];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+    if (more) store_chunk((it & 1) ? Gs0 : Gs1, (it & 1) ? Xs0 : Xs1);
+    __syncthreads();
+  }
+
+  // slab[split][co][col]
+  float* S = slab + (size_t)split * Cout * Ktot;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + wn * NJ * 32 + j * 32 + l32;
+      if (col >= Ktot) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        if (co < Cout) S[(size_t)co * Ktot + col] = acc[i][j][r];
+      }
+    }
+}
+
+// dW = (accumulate ? dW : 0) + sum_s slab[s], summed in split order (deterministic).
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, size_t count,
+                                   float* __restrict__ out, int accumulate) {
+  const size_t n4 = count / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float4 s = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < splits; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * count)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+}
+
+// ======================================================================= helpers
+// Wk[(ci*KK + s)][co] = W[co][ci][s]   (forward operand, K-major)
+__global__ void pack_fwd_kernel(const float* __restrict__ Wt, float* __restrict__ Wk, int Cout,
+                                int Ktot) {
+  const size_t total = (size_t)Cout * Ktot;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Cout);
+    const size_t k = i / Cout;
+    Wk[i] = Wt[(size_t)co * Ktot + k];
+  }
+}
+
+// Wd[(co*KK + s')][ci] = W[co][ci][KK-1-s']   (dgrad operand: transposed + flipped)
+__global__ void pack_dgrad_kernel(const float* __restrict__ Wt, float* __restrict__ Wd, int Cout,
+                                  int Cin, int KK) {
+  const size_t total = (size_t)Cout * Cin * KK;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Cin);
+    const size_t r = i / Cin;
+    const int s = (int)(r % KK);
+    const int co = (int)(r / KK);
+    Wd[i] = Wt[((size_t)co * Cin + ci) * KK + (KK - 1 - s)];
+  }
+}
+
+// G = dY * (Y > 0) (when Y given), db[co] (+)= sum over n,p of G.  grid (Cout, N).
+__global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restrict__ dY,
+                                                            const float* __restrict__ Y,
+                                                            float* __restrict__ G,
+                                                            float* __restrict__ db, int Cout,
+                                                            int HW) {
+  const int co = blockIdx.x, n = blockIdx.y;
+  const size_t base = ((size_t)n * Cout + co) * HW;
+  float s = 0.f;
+  const bool vec = (HW % 4) == 0;
+  if (vec) {
+    const float4* d4 = reinterpret_cast<const float4*>(dY + base);
+    const float4* y4 = Y ? reinterpret_cast<const float4*>(Y + base) : nullptr;
+    float4* g4 = reinterpret_cast<float4*>(G + base);
+    for (int i = threadIdx.x; i < HW / 4; i += 256) {
+      float4 d = d4[i];
+      if (y4) {
+        const float4 y = y4[i];
+        d.x = y.x > 0.f ? d.x : 0.f; d.y = y.y > 0.f ? d.y : 0.f;
+        d.z = y.z > 0.f ? d.z : 0.f; d.w = y.w > 0.f ? d.w : 0.f;
+      }
+      if (G != dY || y4) g4[i] = d;
+      s += (d.x + d.y) + (d.z + d.w);
+    }
+  } else {
+    for (int i = threadIdx.x; i < HW; i += 256) {
+      float d = dY[base + i];
+      if (Y) d = Y[base + i] > 0.f ? d : 0.f;
+      G[base + i] = d;
+      s += d;
+    }
+  }
+  if (!db) return;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+  __shared__ float ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(db + co, (ws[0] + ws[1]) + (ws[2] + ws[3]));
+}
+
+// ======================================================================= launchers
+template <int WM, int WN, int MI, int NJ, int CK, int KS>
+static int launch_fwd(const float* X, const float* Wk, const float* bias, float* Y, int N,
+                      int Cin, int H, int W, int Cout, int relu, hipStream_t s) {
+  using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
+  const int tiles_m = div_up(Cout, C::BM), tiles_w = div_up(W, C::TW), tiles_h = div_up(H, C::TH);
+  const long long nwg = (long long)tiles_m * tiles_w * tiles_h * N;
+  TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
+  const size_t lds = C::LDS_FLOATS * sizeof(float);
+  auto kern = conv_fwd_kernel<WM, WN, MI, NJ, CK, KS>;
+  static bool attr = false;
+  if (!attr) {
+    TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wk, bias, Y, N, Cin, H, W,
+                     Cout, relu, tiles_m, tiles_w, tiles_h);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias, float* Y, int N,
+                             int Cin, int H, int W, int Cout, int KS, int relu, hipStream_t s) {
+  TLOD_CHECK_ARG(Cout % 4 == 0, "Cout must be a multiple of 4");
+  if (KS == 3) {
+    if (Cout <= 64) return launch_fwd<1, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd<2, 2, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+  }
+  if (KS == 1) {
+    if (Cout <= 64) return launch_fwd<1, 4, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd<2, 2, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+  }
+  set_error("conv: only 1x1 and 3x3 kernels (stride 1) are implemented");
+  return kUnsupported;
+}
+
+template <int WM, int WN, int MI, int NJ, int KS>
+static int launch_wgrad(const float* G, const float* X, float* slab, int splits, int N, int Cin,
+                        int H, int W, int Cout, hipStream_t s) {
+  using C = WgCfg<WM, WN, MI, NJ, KS>;
+  const int Ktot = Cin * C::KK;
+  const int tiles_m = div_up(Cout, C::BM), tiles_n = div_up(Ktot, C::BN);
+  const int total_chunks = N * div_up(H, C::TH) * div_up(W, C::TW);
+  const int cps = div_up(total_chunks, splits);
+  const int nwg = tiles_m * tiles_n * splits;
+  const size_t lds = C::LDS_FLOATS * sizeof(float);
+  auto kern = conv_wgrad_kernel<WM, WN, MI, NJ, KS>;
+  static bool attr = false;
+  if (!attr) {
+    TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), lds, s, G, X, slab, N, Cin, H, W, Cout, tiles_m,
+                     tiles_n, splits, cps);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+int wgrad_splits(int N, int Cin, int H, int W, int Cout, int KS) {
+  const int tiles = div_up(Cout, 128) * div_up(Cin * KS * KS, 128);
+  const int chunks = N * div_up(H, 2) * div_up(W, 32);
+  int splits = std::max(1, std::min(chunks / 8, div_up(1024, tiles)));
+  return std::min(splits, 64);
+}
+
+}  // namespace tlod
+
+using namespace tlod;
+
+extern "C" int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
+                                      tlod_stream_t stream) {
+  TLOD_CHECK_ARG(Cout > 0 && Cin > 0 && KS > 0, "bad shape");
+  const size_t total = (size_t)Cout * Cin * KS * KS;
+  hipLaunchKernelGGL(pack_fwd_kernel, dim3((unsigned)std::min<size_t>(div_up((int)std::min<size_t>(total, 1u << 30), 256), 4096)),
+                     dim3(256), 0, (hipStream_t)stream, weight, wk, Cout, Cin * KS * KS);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, int KS, float* wd,
+                                        tlod_stream_t stream) {
+  TLOD_CHECK_ARG(Cout > 0 && Cin > 0 && KS > 0, "bad shape");
+  const size_t total = (size_t)Cout * Cin * KS * KS;
+  hipLaunchKernelGGL(pack_dgrad_kernel, dim3((unsigned)std::min<size_t>(div_up((int)std::min<size_t>(total, 1u << 30), 256), 4096)),
+                     dim3(256), 0, (hipStream_t)stream, weight, wd, Cout, Cin, KS * KS);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_conv_fwd_f32(const float* x, const float* wk, const float* bias, float* y,
+                                 int N, int Cin, int H, int W, int Cout, int KS, int relu,
+                                 tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
+  return conv_fwd_dispatch(x, wk, bias, y, N, Cin, H, W, Cout, KS, relu, (hipStream_t)stream);
+}
+
+extern "C" int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, int N, int Cin,
+                                   int H, int W, int Cout, int KS, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
+  // dx[n, ci] = sum_{co, s'} Wd[(co, s')][ci] * dy[n, co, p + s' - pad]: forward form
+  return conv_fwd_dispatch(dy, wd, nullptr, dx, N, Cout, H, W, Cin, KS, 0, (hipStream_t)stream);
+}
+
+extern "C" size_t tlod_conv_wgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS) {
+  return (size_t)wgrad_splits(N, Cin, H, W, Cout, KS) * Cout * Cin * KS * KS * sizeof(float);
+}
+
+extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, int accumulate,
+                                   int N, int Cin, int H, int W, int Cout, int KS, void* ws,
+                                   size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
+  TLOD_CHECK_ARG((Cout * Cin * KS * KS) % 4 == 0, "Cout*Cin*KS*KS must be a multiple of 4");
+  hipStream_t s = (hipStream_t)stream;
+  const int splits = wgrad_splits(N, Cin, H, W, Cout, KS);
+  if (ws_bytes < (size_t)splits * Cout * Cin * KS * KS * sizeof(float)) {
+    set_error("tlod_conv_wgrad_f32: workspace too small");
+    return kWorkspace;
+  }
+  float* slab = static_cast<float*>(ws);
+  int st;
+  if (KS == 3) st = launch_wgrad<2, 2, 2, 2, 3>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
+  else if (KS == 1) st = launch_wgrad<2, 2, 2, 2, 1>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
+  else { set_error("conv wgrad: only 1x1 and 3x3"); return kUnsupported; }
+  if (st) return st;
+  const size_t count = (size_t)Cout * Cin * KS * KS;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count / 4 + 255) / 256, 2048)),
+                     dim3(256), 0, s, slab, splits, count, dw, accumulate);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db,
+                                      int N, int C, int HW, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0, "bad shape");
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C, N), dim3(256), 0, (hipStream_t)stream, dy, y, g,
+                     db, C, HW);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}

@@ -1,0 +1,150 @@
+"""Backbone / RPN convolution on libtlod's MFMA implicit-GEMM kernels.
+
+``Conv2d`` is a drop-in for the ``nn.Conv2d`` modules inside the reference's
+``RCNN_base`` (torchvision vgg16().features, lib/DAF/vgg16.py:49) and ``RPN_Conv``
+(lib/model/rpn/rpn.py:28): same parameters, same state_dict keys, same default
+shapes.  ``relu=True`` fuses the following ``nn.ReLU`` into the kernel epilogue (the
+backward then applies the ReLU mask from the saved output).
+
+Forward, input-gradient and weight-gradient all run in libtlod (tlod_conv_*_f32).
+Weight gradient is only computed when the weight requires grad, input gradient only
+when the input does (conv3_1 of VGG16 needs no dgrad: its input comes from frozen
+layers, lib/DAF/vgg16.py:52-53).
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _check(x, w):
+    _lib.require_cuda(x, w)
+    if x.dtype != torch.float32 or w.dtype != torch.float32:
+        raise TypeError("tlod conv computes in fp32 (the reference's dtype)")
+
+
+def pack_fwd(weight):
+    Cout, Cin, KS, _ = weight.shape
+    wk = torch.empty((Cin * KS * KS, Cout), dtype=torch.float32, device=weight.device)
+    _lib.check(_lib.lib().tlod_conv_pack_fwd_f32(_lib.ptr(weight.detach().contiguous()), Cout,
+                                                 Cin, KS, _lib.ptr(wk), _lib.stream_of(weight)),
+               "conv_pack_fwd")
+    return wk
+
+
+def pack_dgrad(weight):
+    Cout, Cin, KS, _ = weight.shape
+    wd = torch.empty((Cout * KS * KS, Cin), dtype=torch.float32, device=weight.device)
+    _lib.check(_lib.lib().tlod_conv_pack_dgrad_f32(_lib.ptr(weight.detach().contiguous()), Cout,
+                                                   Cin, KS, _lib.ptr(wd), _lib.stream_of(weight)),
+               "conv_pack_dgrad")
+    return wd
+
+
+def conv_fwd(x, weight, bias=None, relu=False, wk=None):
+    _check(x, weight)
+    x = x.contiguous()
+    N, Cin, H, W = x.shape
+    Cout, _, KS, _ = weight.shape
+    wk = pack_fwd(weight) if wk is None else wk
+    y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
+    b = bias.detach().contiguous() if bias is not None else None
+    _lib.check(_lib.lib().tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N,
+                                            Cin, H, W, Cout, KS, int(relu), _lib.stream_of(x)),
+               "conv_fwd")
+    return y
+
+
+def conv_dgrad(g, weight, wd=None):
+    g = g.contiguous()
+    N, Cout, H, W = g.shape
+    _, Cin, KS, _ = weight.shape
+    wd = pack_dgrad(weight) if wd is None else wd
+    dx = torch.empty((N, Cin, H, W), dtype=torch.float32, device=g.device)
+    _lib.check(_lib.lib().tlod_conv_dgrad_f32(_lib.ptr(g), _lib.ptr(wd), _lib.ptr(dx), N, Cin, H, W,
+                                              Cout, KS, _lib.stream_of(g)), "conv_dgrad")
+    return dx
+
+
+def conv_wgrad(g, x, KS, out=None, accumulate=False):
+    g = g.contiguous()
+    x = x.contiguous()
+    N, Cout, H, W = g.shape
+    Cin = x.shape[1]
+    L = _lib.lib()
+    dw = out if out is not None else torch.empty((Cout, Cin, KS, KS), dtype=torch.float32,
+                                                 device=g.device)
+    ws = _lib.workspace(L.tlod_conv_wgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "wgrad")
+    _lib.check(L.tlod_conv_wgrad_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin,
+                                     H, W, Cout, KS, _lib.ptr(ws), ws.numel(), _lib.stream_of(g)),
+               "conv_wgrad")
+    return dw
+
+
+def relu_bwd_bias(dy, y=None, want_db=True):
+    """g = dy * (y > 0) (y None: g = dy); db = sum_{n,h,w} g."""
+    dy = dy.contiguous()
+    N, C, H, W = dy.shape
+    g = torch.empty_like(dy) if y is not None else dy
+    db = torch.zeros(C, dtype=torch.float32, device=dy.device) if want_db else None
+    _lib.check(_lib.lib().tlod_relu_bwd_bias_f32(_lib.ptr(dy), _lib.ptr(y.contiguous() if y is not None else None),
+                                                 _lib.ptr(g), _lib.ptr(db), N, C, H * W,
+                                                 _lib.stream_of(dy)), "relu_bwd_bias")
+    return g, db
+
+
+class ConvFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        y = conv_fwd(x, weight, bias, relu)
+        ctx.relu = bool(relu)
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], \
+            ctx.has_bias and ctx.needs_input_grad[2]
+        g, db = relu_bwd_bias(dy, y if ctx.relu else None, want_db=need_b)
+        dx = conv_dgrad(g, weight) if need_x else None
+        dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
+        return dx, dw, db, None
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d-compatible (stride 1, padding k//2) with the libtlod kernels; optional
+    fused ReLU."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=None, bias=True,
+                 relu=False):
+        k = kernel_size if isinstance(kernel_size, int) else kernel_size[0]
+        padding = k // 2 if padding is None else padding
+        super().__init__(in_channels, out_channels, k, stride=stride, padding=padding, bias=bias)
+        if stride != 1 or padding != k // 2 or k not in (1, 3):
+            raise NotImplementedError("tlod.Conv2d: stride 1, 'same' padding, 1x1/3x3 only")
+        self.relu = relu
+
+    def forward(self, x):
+        if self.out_channels % 4:
+            # GEMM-library path for the tiny 1x1 heads (e.g. 512->2 of _ImageDA.Conv2)
+            assert self.kernel_size[0] == 1
+            y = F.linear(x.permute(0, 2, 3, 1), self.weight.view(self.out_channels, -1), self.bias)
+            y = y.permute(0, 3, 1, 2).contiguous()
+            return F.relu(y) if self.relu else y
+        return ConvFunction.apply(x, self.weight, self.bias, self.relu)
+
+    def extra_repr(self):
+        return super().extra_repr() + (", relu=True" if self.relu else "")
+
+
+def vgg_init_(conv):
+    """torchvision 0.2.1 VGG init (reference requirements.txt:1): N(0, sqrt(2/(k*k*out))), bias 0."""
+    n = conv.kernel_size[0] * conv.kernel_size[1] * conv.out_channels
+    conv.weight.data.normal_(0, math.sqrt(2.0 / n))
+    if conv.bias is not None:
+        conv.bias.data.zero_()
