@@ -1,0 +1,150 @@
+"""Throughput benchmark of the DAF VGG16 Cityscapes->Foggy training step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+One step = one DAF iteration on one source + one target image (600x1200, synthetic,
+resident in HBM) per GPU: forward, loss, backward (+ RCCL gradient all-reduce for N>1),
+clip_gradient(10), SGD.  value = source images/s over the whole job (max-over-ranks
+step time).  Rank 0 prints one JSON line; see DESIGN.md §Measurement for the roofline
+and cpu_baseline fields.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "transfer-learning-library-for-object-detection_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = ("training images/sec (whole node) DAF VGG16 Cityscapes→Foggy, bs=1/img/GPU at "
+          "1/2/4/8 MI355X")
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--height", type=int, default=600)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=2,
+                    help="oracle CPU steps timed on rank 0 at N=1 (0 disables)")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    return ap.parse_args()
+
+
+def conv_roofline(records):
+    """Aggregate the timed conv launches: algorithmic FLOPs / measured kernel time."""
+    tot_f, tot_ms, by = 0.0, 0.0, {}
+    for s, e, flops, kind in records:
+        ms = s.elapsed_time(e)
+        tot_f += flops
+        tot_ms += ms
+        d = by.setdefault(kind, [0.0, 0.0, 0])
+        d[0] += flops
+        d[1] += ms
+        d[2] += 1
+    if tot_ms == 0:
+        return 0.0, {}, 0.0, 0.0, 0
+    achieved = tot_f / (tot_ms * 1e-3) / 1e12
+    detail = {k: {"launches": v[2], "ms": round(v[1], 3), "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
+              for k, v in by.items()}
+    return achieved, detail, tot_ms, tot_f, len(records)
+
+
+def cpu_baseline(steps, H, W):
+    """The oracle's CPU DAF step (test-infrastructure restatement) on this host's cores."""
+    import oracle.daf_step as ods
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(threads, 64))
+    torch.set_num_threads(threads)
+    t = ods.time_cpu_steps(steps, H, W)
+    return {"value": round(1.0 / t, 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} DAF-VGG16 steps (1 src + 1 tgt image {H}x{W}, synthetic) of the "
+                      f"oracle restatement: numpy RPN/NMS/RoIAlign + torch-CPU fp32 conv/linear; "
+                      f"mean s/step = {t:.2f}"}
+
+
+def main():
+    a = parse()
+    from tlod.dist import GradBucketReducer, init_from_env
+    from tlod import conv as tconv
+    from tlod.detector.train import (SyntheticCityscapes, build_daf_vgg16, make_optimizer,
+                                     train_step)
+
+    rank, world = init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    model = build_daf_vgg16(dev)
+    opt = make_optimizer(model, 2e-3)
+    reducer = GradBucketReducer(model, bucket_mb=a.bucket_mb) if world > 1 else None
+    data = SyntheticCityscapes(dev, H=a.height, W=a.width, seed=1000 * rank + 1)
+
+    for _ in range(a.warmup):
+        train_step(model, opt, data.next(), reducer=reducer)
+    torch.cuda.synchronize()
+
+    records = []
+    tconv.PROFILE = records
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = []
+    for _ in range(a.steps):
+        losses.append(train_step(model, opt, data.next(), reducer=reducer))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    tconv.PROFILE = None
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    el = float(elapsed.item())
+    ms_per_step = el / a.steps * 1e3
+    value = world * a.steps / el  # one source image per rank per step
+    last_loss = float(torch.stack(losses).float().mean().item())
+
+    achieved, detail, conv_ms, conv_f, n_launch = conv_roofline(records)
+    result = {
+        "metric": METRIC, "value": round(value, 4), "unit": "img/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "DAF VGG16 Cityscapes->Foggy training step (methods/DAF/DAF_train.py), "
+                               "1 source + 1 target image per GPU per step",
+                   "image_hw": [a.height, a.width], "source_images_per_step": world,
+                   "images_processed_per_step": 2 * world, "parallelism": f"dp{world}",
+                   "classes": 9, "rpn_pre_post_nms_train": [12000, 2000],
+                   "rpn_pre_post_nms_test": [6000, 300], "rcnn_batch": 256},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
+                     "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "tlod conv (fwd+dgrad+wgrad, f32 MFMA implicit GEMM)",
+                     "launches": n_launch, "kernel_ms_per_step": round(conv_ms / a.steps, 3),
+                     "gflop_per_step": round(conv_f / a.steps / 1e9, 2), "by_kind": detail},
+        "mean_loss": round(last_loss, 4),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and a.cpu_baseline_steps > 0:
+        result["cpu_baseline"] = cpu_baseline(a.cpu_baseline_steps, a.height, a.width)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

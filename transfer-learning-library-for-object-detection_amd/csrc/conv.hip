@@ -96,7 +96,17 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
       if (e < C::A_V4) {
         const int kk = e / (C::BM / 4), mm = (e % (C::BM / 4)) * 4;
         const int k = k0 + kk, m = m0 + mm;
-        if (k < Ktot && m < Cout) v = *reinterpret_cast<const float4*>(Wk + (size_t)k * Cout + m);
+        if (k < Ktot && m < Cout) {
+          const float* src = Wk + (size_t)k * Cout + m;
+          if ((Cout & 3) == 0) {
+            v = *reinterpret_cast<const float4*>(src);
+          } else {  // rows not 16-B aligned (e.g. dgrad of a 3-channel input)
+            v.x = src[0];
+            v.y = m + 1 < Cout ? src[1] : 0.f;
+            v.z = m + 2 < Cout ? src[2] : 0.f;
+            v.w = m + 3 < Cout ? src[3] : 0.f;
+          }
+        }
       }
       ra[i] = v;
     }
@@ -459,7 +469,6 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
 
 static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias, float* Y, int N,
                              int Cin, int H, int W, int Cout, int KS, int relu, hipStream_t s) {
-  TLOD_CHECK_ARG(Cout % 4 == 0, "Cout must be a multiple of 4");
   if (KS == 3) {
     if (Cout <= 64) return launch_fwd<1, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
     return launch_fwd<2, 2, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);

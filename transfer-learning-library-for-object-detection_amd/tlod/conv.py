@@ -20,6 +20,21 @@ import torch.nn.functional as F
 from . import _lib
 
 
+# Optional launch timing (bench.py): list of (start_event, end_event, flops, kind) or None.
+PROFILE = None
+
+
+def _timed(kind, flops, fn):
+    if PROFILE is None:
+        return fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    r = fn()
+    e.record()
+    PROFILE.append((s, e, flops, kind))
+    return r
+
+
 def _check(x, w):
     _lib.require_cuda(x, w)
     if x.dtype != torch.float32 or w.dtype != torch.float32:
@@ -52,9 +67,9 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None):
     wk = pack_fwd(weight) if wk is None else wk
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
-    _lib.check(_lib.lib().tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N,
-                                            Cin, H, W, Cout, KS, int(relu), _lib.stream_of(x)),
-               "conv_fwd")
+    _timed("fwd", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
+        _lib.lib().tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N, Cin, H,
+                                     W, Cout, KS, int(relu), _lib.stream_of(x)), "conv_fwd"))
     return y
 
 
@@ -64,8 +79,9 @@ def conv_dgrad(g, weight, wd=None):
     _, Cin, KS, _ = weight.shape
     wd = pack_dgrad(weight) if wd is None else wd
     dx = torch.empty((N, Cin, H, W), dtype=torch.float32, device=g.device)
-    _lib.check(_lib.lib().tlod_conv_dgrad_f32(_lib.ptr(g), _lib.ptr(wd), _lib.ptr(dx), N, Cin, H, W,
-                                              Cout, KS, _lib.stream_of(g)), "conv_dgrad")
+    _timed("dgrad", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
+        _lib.lib().tlod_conv_dgrad_f32(_lib.ptr(g), _lib.ptr(wd), _lib.ptr(dx), N, Cin, H, W, Cout,
+                                       KS, _lib.stream_of(g)), "conv_dgrad"))
     return dx
 
 
@@ -78,9 +94,9 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False):
     dw = out if out is not None else torch.empty((Cout, Cin, KS, KS), dtype=torch.float32,
                                                  device=g.device)
     ws = _lib.workspace(L.tlod_conv_wgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "wgrad")
-    _lib.check(L.tlod_conv_wgrad_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin,
-                                     H, W, Cout, KS, _lib.ptr(ws), ws.numel(), _lib.stream_of(g)),
-               "conv_wgrad")
+    _timed("wgrad", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
+        L.tlod_conv_wgrad_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin, H, W,
+                              Cout, KS, _lib.ptr(ws), ws.numel(), _lib.stream_of(g)), "conv_wgrad"))
     return dw
 
 

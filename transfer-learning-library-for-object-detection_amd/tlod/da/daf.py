@@ -1,0 +1,258 @@
+"""DAF (Domain Adaptive Faster R-CNN) on the tlod kernels — lib/DAF/{DA,faster_rcnn,vgg16}.py.
+
+``vgg16(classes).create_architecture()`` then ``model(im_data, im_info, gt_boxes,
+num_boxes, need_backprop, tgt_im_data, tgt_im_info, tgt_gt_boxes, tgt_num_boxes,
+tgt_need_backprop)`` returns the reference's 14-tuple (lib/DAF/faster_rcnn.py:222-223).
+
+Execution differs from the reference only in scheduling, not in math:
+  * source and target images share one backbone / RPN-conv / RoIAlign / head pass
+    (batched along N) when their sizes match — every op is per-image, so the results
+    are the same as two passes (the reference runs RCNN_base twice, :58 and :137);
+  * the DA label layers (LabelResizeLayer.py:18-57: D2H, cv2.resize, H2D) become
+    on-device constant fills, including the reference's instance-label quirk (target
+    RoIs 256.. get label 1 because only the first 256 rows are overwritten, :48-55);
+  * no host synchronisation anywhere in the step (nonzero / .item() / numpy RNG are
+    replaced by device-side equivalents, see tlod.rpn).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..config import cfg
+from ..conv import Conv2d
+from ..detector.losses import smooth_l1_loss
+from ..detector.vgg16 import vgg16_base, vgg16_top
+from ..roi_align import RoIAlignAvg
+from ..roi_pool import _RoIPooling
+from ..rpn.proposal_target import _ProposalTargetLayer
+from ..rpn.rpn_head import _RPN
+
+
+class GRLayer(torch.autograd.Function):
+    """Gradient reversal (lib/DAF/DA.py:19-33): identity forward, -alpha * grad backward."""
+
+    @staticmethod
+    def forward(ctx, x, alpha=0.1):
+        ctx.alpha = alpha
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.neg() * ctx.alpha, None
+
+
+def grad_reverse(x, alpha=0.1):
+    return GRLayer.apply(x, alpha)
+
+
+def image_label(score, need_backprop):
+    """ImageLabelResizeLayer (LabelResizeLayer.py:18-38): (B,H,W) long filled with the
+    per-image need_backprop — on device."""
+    B, _, H, W = score.shape
+    return need_backprop.view(-1, 1, 1).to(score.device).long().expand(B, H, W)
+
+
+def instance_label(n_rows, need_backprop, minibatch=256):
+    """InstanceLabelResizeLayer (LabelResizeLayer.py:41-57): ones, then rows
+    [i*256, (i+1)*256) := need_backprop[i] (rows past B*256 stay 1)."""
+    nb = need_backprop.view(-1).float()
+    y = torch.ones((n_rows, 1), dtype=torch.float32, device=nb.device)
+    for i in range(nb.numel()):
+        y[i * minibatch:(i + 1) * minibatch] = nb[i]
+    return y
+
+
+class _ImageDA(nn.Module):
+    """lib/DAF/DA.py:36-50: GRL -> 1x1 dim->512 -> ReLU -> 1x1 512->2 (no biases)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.Conv1 = Conv2d(dim, 512, 1, bias=False, relu=True)
+        self.Conv2 = Conv2d(512, 2, 1, bias=False)
+
+    def forward(self, x, need_backprop):
+        x = self.Conv2(self.Conv1(grad_reverse(x)))
+        return x, image_label(x, need_backprop)
+
+
+class _InstanceDA(nn.Module):
+    """lib/DAF/DA.py:53-73: GRL -> fc 1024 -> fc 1024 -> fc 1 -> sigmoid.
+
+    ``in_dim`` is 4096 for VGG16 (the reference hard-codes 4096, which breaks its
+    ResNet101 variant whose head emits 2048-d features, lib/DAF/resnet.py:243)."""
+
+    def __init__(self, in_dim=4096):
+        super().__init__()
+        self.dc_ip1 = nn.Linear(in_dim, 1024)
+        self.dc_relu1 = nn.ReLU()
+        self.dc_drop1 = nn.Dropout(p=0.5)
+        self.dc_ip2 = nn.Linear(1024, 1024)
+        self.dc_relu2 = nn.ReLU()
+        self.dc_drop2 = nn.Dropout(p=0.5)
+        self.clssifer = nn.Linear(1024, 1)
+
+    def forward(self, x, need_backprop):
+        x = grad_reverse(x)
+        x = self.dc_drop1(self.dc_relu1(self.dc_ip1(x)))
+        x = self.dc_drop2(self.dc_relu2(self.dc_ip2(x)))
+        x = torch.sigmoid(self.clssifer(x))
+        return x, instance_label(x.shape[0], need_backprop)
+
+
+class _fasterRCNN(nn.Module):
+    """lib/DAF/faster_rcnn.py:22-247."""
+
+    def __init__(self, classes, class_agnostic):
+        super().__init__()
+        self.classes = classes
+        self.n_classes = len(classes)
+        self.class_agnostic = class_agnostic
+        self.RCNN_loss_cls = 0
+        self.RCNN_loss_bbox = 0
+        self.RCNN_rpn = _RPN(self.dout_base_model)
+        self.RCNN_proposal_target = _ProposalTargetLayer(self.n_classes)
+        self.RCNN_roi_pool = _RoIPooling(cfg.POOLING_SIZE, cfg.POOLING_SIZE, 1.0 / 16.0)
+        self.RCNN_roi_align = RoIAlignAvg(cfg.POOLING_SIZE, cfg.POOLING_SIZE, 1.0 / 16.0)
+        self.RCNN_imageDA = _ImageDA(self.dout_base_model)
+        self.RCNN_instanceDA = _InstanceDA(self.instance_dim)
+        self.consistency_loss = nn.MSELoss(reduction="sum")
+        self.replay_rng = None  # tests: np.random-like object -> reference-exact sampling
+
+    # ------------------------------------------------------------------ pieces
+    def _pool(self, feat, rois):
+        if cfg.POOLING_MODE == "align":
+            return self.RCNN_roi_align(feat, rois)
+        if cfg.POOLING_MODE == "pool":
+            return self.RCNN_roi_pool(feat, rois)
+        raise NotImplementedError("POOLING_MODE 'crop' is out of scope (configs use 'align')")
+
+    def _rcnn_losses(self, pooled_s, rois_label, rois_target, rois_inside_ws, rois_outside_ws):
+        bbox_pred = self.RCNN_bbox_pred(pooled_s)
+        if self.training and not self.class_agnostic:
+            view = bbox_pred.view(bbox_pred.size(0), int(bbox_pred.size(1) / 4), 4)
+            bbox_pred = torch.gather(view, 1, rois_label.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
+        cls_score = self.RCNN_cls_score(pooled_s)
+        cls_prob = F.softmax(cls_score, 1)
+        loss_cls = F.cross_entropy(cls_score, rois_label)
+        loss_bbox = smooth_l1_loss(bbox_pred, rois_target, rois_inside_ws, rois_outside_ws)
+        return cls_prob, bbox_pred, loss_cls, loss_bbox
+
+    def _da_losses(self, base_score_s, base_score_t, ins_s, ins_t, need_s, need_t):
+        lab_s = image_label(base_score_s, need_s)
+        lab_t = image_label(base_score_t, need_t)
+        da_img = F.nll_loss(F.log_softmax(base_score_s, 1), lab_s)
+        tgt_da_img = F.nll_loss(F.log_softmax(base_score_t, 1), lab_t)
+        y_s = instance_label(ins_s.shape[0], need_s)
+        y_t = instance_label(ins_t.shape[0], need_t)
+        da_ins = F.binary_cross_entropy(ins_s, y_s)
+        tgt_da_ins = F.binary_cross_entropy(ins_t, y_t)
+        cons_s = F.softmax(base_score_s, 1)[:, 1, :, :].mean()
+        cons_t = F.softmax(base_score_t, 1)[:, 0, :, :].mean()
+        da_cst = self.consistency_loss(ins_s, cons_s.detach().expand_as(ins_s))
+        tgt_da_cst = self.consistency_loss(ins_t, cons_t.detach().expand_as(ins_t))
+        return da_img, da_ins, tgt_da_img, tgt_da_ins, da_cst, tgt_da_cst
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, im_data, im_info, gt_boxes, num_boxes, need_backprop,
+                tgt_im_data, tgt_im_info, tgt_gt_boxes, tgt_num_boxes, tgt_need_backprop):
+        batch_size = im_data.size(0)
+        im_info = im_info.detach()
+        gt_boxes = gt_boxes.detach()
+        same = (im_data.shape == tgt_im_data.shape) and batch_size == 1
+        if same:
+            base2 = self.RCNN_base(torch.cat([im_data, tgt_im_data], 0))
+            base_feat, tgt_base_feat = base2[:1], base2[1:]
+            score2, score_r2, prob2, bbox2 = self.RCNN_rpn.head(base2)
+            s_score, s_score_r, s_prob, s_bbox = score2[:1], score_r2[:1], prob2[:1], bbox2[:1]
+            t_prob, t_bbox = prob2[1:], bbox2[1:]
+        else:
+            base_feat = self.RCNN_base(im_data)
+            tgt_base_feat = self.RCNN_base(tgt_im_data)
+            s_score, s_score_r, s_prob, s_bbox = self.RCNN_rpn.head(base_feat)
+            _, _, t_prob, t_bbox = self.RCNN_rpn.head(tgt_base_feat)
+
+        # source RPN in train mode (faster_rcnn.py:62-63)
+        rpn = self.RCNN_rpn
+        rois = rpn.RPN_proposal((s_prob.detach(), s_bbox.detach(), im_info, "TRAIN"))
+        rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes, im_info,
+                                                    num_boxes, rng=self.replay_rng)
+        # target RPN in eval mode (faster_rcnn.py:140-142): TEST proposals, no losses
+        tgt_rois = rpn.RPN_proposal((t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST"))
+
+        rois, rois_label, rois_target, rois_inside_ws, rois_outside_ws = \
+            self.RCNN_proposal_target(rois, gt_boxes, num_boxes, rng=self.replay_rng)
+        rois_label = rois_label.view(-1).long()
+        rois_target = rois_target.view(-1, rois_target.size(2))
+        rois_inside_ws = rois_inside_ws.view(-1, rois_inside_ws.size(2))
+        rois_outside_ws = rois_outside_ws.view(-1, rois_outside_ws.size(2))
+
+        n_s = rois.size(1)
+        if same:
+            t_rois = tgt_rois.view(-1, 5).clone()
+            t_rois[:, 0] = 1.0  # target image is batch entry 1 of base2
+            pooled2 = self._pool(base2, torch.cat([rois.view(-1, 5), t_rois], 0))
+            feat2 = self._head_to_tail(pooled2)
+            pooled_feat, tgt_pooled_feat = feat2[:n_s], feat2[n_s:]
+        else:
+            pooled_feat = self._head_to_tail(self._pool(base_feat, rois.view(-1, 5)))
+            tgt_pooled_feat = self._head_to_tail(self._pool(tgt_base_feat, tgt_rois.view(-1, 5)))
+
+        cls_prob, bbox_pred, RCNN_loss_cls, RCNN_loss_bbox = self._rcnn_losses(
+            pooled_feat, rois_label, rois_target, rois_inside_ws, rois_outside_ws)
+        cls_prob = cls_prob.view(batch_size, n_s, -1)
+        bbox_pred = bbox_pred.view(batch_size, n_s, -1)
+
+        # DA heads (faster_rcnn.py:181-220)
+        if same:
+            score_img2, _ = self.RCNN_imageDA(base2, need_backprop.new_ones(2))
+            base_score, tgt_base_score = score_img2[:1], score_img2[1:]
+            ins2, _ = self.RCNN_instanceDA(feat2, need_backprop.new_ones(1))
+            ins_s, ins_t = ins2[:n_s], ins2[n_s:]
+        else:
+            base_score, _ = self.RCNN_imageDA(base_feat, need_backprop)
+            tgt_base_score, _ = self.RCNN_imageDA(tgt_base_feat, tgt_need_backprop)
+            ins_s, _ = self.RCNN_instanceDA(pooled_feat, need_backprop)
+            ins_t, _ = self.RCNN_instanceDA(tgt_pooled_feat, tgt_need_backprop)
+        da = self._da_losses(base_score, tgt_base_score, ins_s, ins_t, need_backprop,
+                             tgt_need_backprop)
+        DA_img_loss_cls, DA_ins_loss_cls, tgt_DA_img_loss_cls, tgt_DA_ins_loss_cls, \
+            DA_cst_loss, tgt_DA_cst_loss = da
+        return (rois, cls_prob, bbox_pred, rpn_loss_cls, rpn_loss_bbox, RCNN_loss_cls,
+                RCNN_loss_bbox, rois_label, DA_img_loss_cls, DA_ins_loss_cls, tgt_DA_img_loss_cls,
+                tgt_DA_ins_loss_cls, DA_cst_loss, tgt_DA_cst_loss)
+
+    def _init_weights(self):
+        """faster_rcnn.py:227-243 (normal_init, truncated=False)."""
+        def normal_init(m, mean, std):
+            m.weight.data.normal_(mean, std)
+            m.bias.data.zero_()
+        normal_init(self.RCNN_rpn.RPN_Conv, 0, 0.01)
+        normal_init(self.RCNN_rpn.RPN_cls_score, 0, 0.01)
+        normal_init(self.RCNN_rpn.RPN_bbox_pred, 0, 0.01)
+        normal_init(self.RCNN_cls_score, 0, 0.01)
+        normal_init(self.RCNN_bbox_pred, 0, 0.001)
+
+    def create_architecture(self):
+        self._init_modules()
+        self._init_weights()
+
+
+class vgg16(_fasterRCNN):
+    """lib/DAF/vgg16.py:20-71 (random init: pretrained caffe weights are external)."""
+
+    def __init__(self, classes, pretrained=False, class_agnostic=False):
+        self.dout_base_model = 512
+        self.instance_dim = 4096
+        self.pretrained = pretrained
+        self.class_agnostic = class_agnostic
+        _fasterRCNN.__init__(self, classes, class_agnostic)
+
+    def _init_modules(self):
+        self.RCNN_base = vgg16_base()
+        self.RCNN_top = vgg16_top()
+        self.RCNN_cls_score = nn.Linear(4096, self.n_classes)
+        self.RCNN_bbox_pred = nn.Linear(4096, 4 if self.class_agnostic else 4 * self.n_classes)
+
+    def _head_to_tail(self, pool5):
+        return self.RCNN_top(pool5.view(pool5.size(0), -1))

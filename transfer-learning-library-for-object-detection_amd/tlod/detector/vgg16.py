@@ -1,0 +1,39 @@
+"""VGG16 backbone and head for the DAF/MAF/ATF detectors (lib/DAF/vgg16.py:20-71).
+
+``RCNN_base`` keeps torchvision vgg16().features[:-1] indices (so state_dict keys are
+``RCNN_base.{0,2,5,...}.weight/bias`` as in the reference) with every conv+ReLU pair
+fused into one libtlod conv (the ReLU slots become nn.Identity).  Layers 0-9 (conv1_x,
+conv2_x) are frozen (vgg16.py:52-53).  ``RCNN_top`` = classifier[:-1]:
+Linear(25088,4096) ReLU Dropout Linear(4096,4096) ReLU Dropout (hipBLASLt GEMMs).
+"""
+import torch.nn as nn
+
+from ..conv import Conv2d, vgg_init_
+
+# torchvision vgg16 cfg "D"
+VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512]
+
+
+def vgg16_base(frozen_layers=10):
+    layers, cin = [], 3
+    for v in VGG16_CFG:
+        if v == "M":
+            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+        else:
+            conv = Conv2d(cin, v, 3, relu=True)
+            vgg_init_(conv)
+            layers += [conv, nn.Identity()]  # index of the fused ReLU stays occupied
+            cin = v
+    base = nn.Sequential(*layers)  # features[:-1]: the last max-pool is not used
+    for i in range(frozen_layers):
+        for p in base[i].parameters():
+            p.requires_grad = False
+    return base
+
+
+def vgg16_top():
+    fc6, fc7 = nn.Linear(512 * 7 * 7, 4096), nn.Linear(4096, 4096)
+    for m in (fc6, fc7):  # torchvision VGG Linear init
+        m.weight.data.normal_(0, 0.01)
+        m.bias.data.zero_()
+    return nn.Sequential(fc6, nn.ReLU(True), nn.Dropout(), fc7, nn.ReLU(True), nn.Dropout())

@@ -1,0 +1,106 @@
+"""Data parallelism for the DAF step: one process per GPU, RCCL all-reduce over xGMI.
+
+Replaces the reference's single-process ``nn.DataParallel`` (methods/DAF/DAF_train.py:
+341-342), which at ``--bs 1`` never runs more than one replica and reduces gradients to
+GPU 0 through the host thread.  Here:
+
+  * parameters are broadcast from rank 0 once at start;
+  * every trainable parameter's ``.grad`` is a view into a flat, bucket-contiguous
+    buffer, so autograd accumulates straight into the buffers RCCL reduces;
+  * a post-accumulate-grad hook counts ready parameters per bucket and launches an async
+    all-reduce (ReduceOp.AVG on RCCL — the DataParallel loss.mean() semantics) as soon
+    as a bucket is complete, overlapping communication with the rest of the backward
+    (the large fc6/fc7 buckets complete first: the heads backprop before the backbone);
+  * ``finish()`` waits for the outstanding buckets before clip_gradient / SGD, which
+    then run on identical gradients on every rank (no extra collective for the norm).
+
+Bucket sizing targets point-to-point xGMI rings: few, large messages (default 64 MB).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torch.distributed.run)."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        return 0, 1
+    rank = int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            device_id=torch.device("cuda", local) if backend == "nccl" else None)
+    return rank, world
+
+
+class GradBucketReducer:
+    def __init__(self, model, bucket_mb=64.0, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        backend = dist.get_backend(group)
+        self.avg = backend == "nccl"
+        # broadcast initial weights (and buffers) from rank 0
+        with torch.no_grad():
+            for t in list(model.parameters()) + list(model.buffers()):
+                dist.broadcast(t.data, 0, group=group)
+        # buckets in reverse registration order (~ gradient readiness order)
+        cap = int(bucket_mb * 1024 * 1024 / 4)
+        buckets, cur, cur_n = [], [], 0
+        for p in reversed(self.params):
+            if cur and cur_n + p.numel() > cap:
+                buckets.append(cur)
+                cur, cur_n = [], 0
+            cur.append(p)
+            cur_n += p.numel()
+        if cur:
+            buckets.append(cur)
+        self.buckets = []
+        self.bucket_of = {}
+        for bi, ps in enumerate(buckets):
+            n = sum(p.numel() for p in ps)
+            flat = torch.zeros(n, dtype=ps[0].dtype, device=ps[0].device)
+            off = 0
+            for p in ps:
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                self.bucket_of[p] = bi
+                off += p.numel()
+            self.buckets.append({"flat": flat, "params": ps, "ready": 0, "work": None})
+        self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def zero_grad(self):
+        for b in self.buckets:
+            b["flat"].zero_()
+            b["ready"] = 0
+            b["work"] = None
+
+    def _launch(self, b):
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        b["work"] = dist.all_reduce(b["flat"], op=op, group=self.group, async_op=True)
+
+    def _on_grad(self, p):
+        b = self.buckets[self.bucket_of[p]]
+        b["ready"] += 1
+        if b["ready"] == len(b["params"]):
+            self._launch(b)
+
+    def finish(self):
+        for b in self.buckets:
+            if b["work"] is None:
+                self._launch(b)
+        for b in self.buckets:
+            b["work"].wait()
+            if not self.avg:
+                b["flat"].div_(self.world)
+            b["work"] = None
+            b["ready"] = 0
+        # grads must still alias the flat buffers (optimizer.zero_grad(set_to_none=False))
+        for p in self.params:
+            assert p.grad is not None
