@@ -1,0 +1,221 @@
+"""Oracle: the DAF VGG16 training step on the CPU (test infrastructure + bench.py's
+cpu_baseline leg only).
+
+A restatement of lib/DAF/faster_rcnn.py:45-224 + methods/DAF/DAF_train.py:384-408 in
+plain torch-CPU fp32 (conv/linear/pool/softmax — the third-party arithmetic the reference
+gets from PyTorch, "parity unpinned" at that boundary) with the numpy restatements of the
+reference's own ops (oracle.rpn / oracle.roi / oracle.nms).  Module names mirror the
+reference's state_dict keys so weights can be copied from the GPU model.
+"""
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import roi as oroi
+from . import rpn as orpn
+
+VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512]
+CFG = dict(pre_train=12000, post_train=2000, pre_test=6000, post_test=300, nms=0.7,
+           scales=(4, 8, 16, 32), ratios=(0.5, 1, 2), stride=16, pool=7, lamda=0.1)
+
+
+class _RoIAlignAvgCPU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois):
+        f = feat.detach().numpy()
+        r = rois.detach().numpy()
+        ctx.meta = (r, f.shape)
+        return torch.from_numpy(oroi.roi_align_avg_fwd(f, r, CFG["pool"], CFG["pool"], 1 / 16))
+
+    @staticmethod
+    def backward(ctx, g):
+        r, (B, C, H, W) = ctx.meta
+        return torch.from_numpy(oroi.roi_align_avg_bwd(g.numpy(), r, B, C, H, W, 1 / 16)), None
+
+
+class _GRL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, alpha):
+        ctx.alpha = alpha
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.neg() * ctx.alpha, None
+
+
+def _smooth_l1(pred, target, iw, ow, sigma=1.0, dim=(1,)):
+    s2 = sigma ** 2
+    d = iw * (pred - target)
+    a = d.abs()
+    sign = (a < 1.0 / s2).float()
+    loss = ow * (d.pow(2) * (s2 / 2.0) * sign + (a - 0.5 / s2) * (1.0 - sign))
+    for i in sorted(dim, reverse=True):
+        loss = loss.sum(i)
+    return loss.mean()
+
+
+class OracleDAF(nn.Module):
+    def __init__(self, n_classes=9, dropout=0.5):
+        super().__init__()
+        layers, cin = [], 3
+        for v in VGG16_CFG:
+            if v == "M":
+                layers.append(nn.MaxPool2d(2, 2))
+            else:
+                layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
+                cin = v
+        self.RCNN_base = nn.Sequential(*layers)
+        for i in range(10):
+            for p in self.RCNN_base[i].parameters():
+                p.requires_grad = False
+        self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), nn.ReLU(True), nn.Dropout(dropout),
+                                      nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout))
+        self.RCNN_cls_score = nn.Linear(4096, n_classes)
+        self.RCNN_bbox_pred = nn.Linear(4096, 4 * n_classes)
+        rpn = nn.Module()
+        rpn.RPN_Conv = nn.Conv2d(512, 512, 3, padding=1)
+        rpn.RPN_cls_score = nn.Conv2d(512, 24, 1)
+        rpn.RPN_bbox_pred = nn.Conv2d(512, 48, 1)
+        self.RCNN_rpn = rpn
+        ida = nn.Module()
+        ida.Conv1 = nn.Conv2d(512, 512, 1, bias=False)
+        ida.Conv2 = nn.Conv2d(512, 2, 1, bias=False)
+        self.RCNN_imageDA = ida
+        ins = nn.Module()
+        ins.dc_ip1, ins.dc_ip2, ins.clssifer = nn.Linear(4096, 1024), nn.Linear(1024, 1024), nn.Linear(1024, 1)
+        self.RCNN_instanceDA = ins
+        self.dropout = dropout
+        self.base_anchors = orpn.make_base_anchors(CFG["scales"], CFG["ratios"])
+
+    def _rpn(self, feat):
+        x = F.relu(self.RCNN_rpn.RPN_Conv(feat))
+        score = self.RCNN_rpn.RPN_cls_score(x)
+        B, C, H, W = score.shape
+        sr = score.view(B, 2, C * H // 2, W)
+        prob = F.softmax(sr, 1).view(B, C, H, W)
+        return score, sr, prob, self.RCNN_rpn.RPN_bbox_pred(x)
+
+    def _image_da(self, feat):
+        x = _GRL.apply(feat, 0.1)
+        return self.RCNN_imageDA.Conv2(F.relu(self.RCNN_imageDA.Conv1(x)))
+
+    def _instance_da(self, x):
+        m = self.RCNN_instanceDA
+        x = _GRL.apply(x, 0.1)
+        x = F.dropout(F.relu(m.dc_ip1(x)), self.dropout, self.training)
+        x = F.dropout(F.relu(m.dc_ip2(x)), self.dropout, self.training)
+        return torch.sigmoid(m.clssifer(x))
+
+    def forward(self, batch, rng, rois_override=None):
+        """rois_override: (source proposals (1,2000,5), target proposals (1,300,5)) taken
+        from the device run, so float-order differences in the score sort cannot fork
+        the sampled RoIs between the two implementations."""
+        (im, info, gt, num, need, t_im, t_info, t_gt, t_num, t_need) = batch
+        c = CFG
+        base = self.RCNN_base(im)
+        score, sr, prob, bbox = self._rpn(base)
+        rois = orpn.proposal_layer(prob.detach().numpy(), bbox.detach().numpy(), info.numpy(),
+                                   self.base_anchors, c["stride"], c["pre_train"], c["post_train"],
+                                   c["nms"])
+        if rois_override is not None:
+            rois = rois_override[0]
+        H, W = score.shape[2:]
+        lab, tgt, iw, ow = orpn.anchor_target(H, W, gt.numpy(), info.numpy(), self.base_anchors,
+                                              c["stride"], rng)
+        lab_t = torch.from_numpy(lab).view(-1)
+        keep = lab_t != -1
+        s2 = sr.permute(0, 2, 3, 1).contiguous().view(-1, 2)
+        rpn_loss_cls = F.cross_entropy(s2[keep], lab_t[keep].long())
+        rpn_loss_box = _smooth_l1(bbox, torch.from_numpy(tgt), torch.from_numpy(iw),
+                                  torch.from_numpy(ow), sigma=3, dim=[1, 2, 3])
+        r, rl, rt, riw, row = orpn.proposal_target(rois, gt.numpy(), rng)
+        rl = torch.from_numpy(rl).view(-1).long()
+        pooled = _RoIAlignAvgCPU.apply(base, torch.from_numpy(r).view(-1, 5))
+        fc7 = self.RCNN_top(pooled.view(pooled.size(0), -1))
+        bp = self.RCNN_bbox_pred(fc7).view(fc7.size(0), -1, 4)
+        bp = torch.gather(bp, 1, rl.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
+        cls = self.RCNN_cls_score(fc7)
+        rcnn_cls = F.cross_entropy(cls, rl)
+        rcnn_box = _smooth_l1(bp, torch.from_numpy(rt).view(-1, 4), torch.from_numpy(riw).view(-1, 4),
+                              torch.from_numpy(row).view(-1, 4))
+        # target image: RPN in eval mode (TEST proposals)
+        t_base = self.RCNN_base(t_im)
+        _, _, t_prob, t_bbox = self._rpn(t_base)
+        t_rois = orpn.proposal_layer(t_prob.detach().numpy(), t_bbox.detach().numpy(),
+                                     t_info.numpy(), self.base_anchors, c["stride"], c["pre_test"],
+                                     c["post_test"], c["nms"])
+        if rois_override is not None:
+            t_rois = rois_override[1]
+        t_pooled = _RoIAlignAvgCPU.apply(t_base, torch.from_numpy(t_rois).view(-1, 5))
+        t_fc7 = self.RCNN_top(t_pooled.view(t_pooled.size(0), -1))
+        # DA (faster_rcnn.py:181-220)
+        bs = self._image_da(base)
+        da_img = F.nll_loss(F.log_softmax(bs, 1), torch.ones(bs.shape[0], *bs.shape[2:], dtype=torch.long))
+        ins = self._instance_da(fc7)
+        da_ins = F.binary_cross_entropy(ins, torch.ones_like(ins))
+        cst = F.softmax(bs, 1)[:, 1].mean().detach()
+        da_cst = ((ins - cst) ** 2).sum()
+        tbs = self._image_da(t_base)
+        t_da_img = F.nll_loss(F.log_softmax(tbs, 1), torch.zeros(tbs.shape[0], *tbs.shape[2:], dtype=torch.long))
+        t_ins = self._instance_da(t_fc7)
+        y = torch.ones_like(t_ins)
+        y[:256] = 0  # InstanceLabelResizeLayer quirk (LabelResizeLayer.py:48-55)
+        t_da_ins = F.binary_cross_entropy(t_ins, y)
+        t_cst = F.softmax(tbs, 1)[:, 0].mean().detach()
+        t_da_cst = ((t_ins - t_cst) ** 2).sum()
+        return dict(rpn_loss_cls=rpn_loss_cls, rpn_loss_box=rpn_loss_box, RCNN_loss_cls=rcnn_cls,
+                    RCNN_loss_bbox=rcnn_box, DA_img_loss_cls=da_img, DA_ins_loss_cls=da_ins,
+                    tgt_DA_img_loss_cls=t_da_img, tgt_DA_ins_loss_cls=t_da_ins, DA_cst_loss=da_cst,
+                    tgt_DA_cst_loss=t_da_cst, rois=r)
+
+
+def total_loss(o, lamda=0.1):
+    return (o["rpn_loss_cls"] + o["rpn_loss_box"] + o["RCNN_loss_cls"] + o["RCNN_loss_bbox"]
+            + lamda * (o["DA_img_loss_cls"] + o["DA_ins_loss_cls"] + o["tgt_DA_img_loss_cls"]
+                       + o["tgt_DA_ins_loss_cls"] + o["DA_cst_loss"] + o["tgt_DA_cst_loss"]))
+
+
+def synthetic_batch(H, W, seed=1, G=8):
+    rng = np.random.default_rng(seed)
+    means = np.array([102.9801, 115.9465, 122.7717], np.float32)
+
+    def img():
+        u8 = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        return torch.from_numpy((u8.astype(np.float32) - means).transpose(2, 0, 1).copy())[None]
+    gt = np.zeros((1, 50, 5), np.float32)
+    x1, y1 = rng.uniform(0, W - 64, G), rng.uniform(0, H - 64, G)
+    w, h = rng.uniform(32, 400, G), rng.uniform(32, 400, G)
+    gt[0, :G, 0], gt[0, :G, 1] = x1, y1
+    gt[0, :G, 2], gt[0, :G, 3] = np.minimum(x1 + w, W - 1), np.minimum(y1 + h, H - 1)
+    gt[0, :G, 4] = rng.integers(1, 9, G)
+    info = torch.tensor([[H, W, 600.0 / 1024.0]])
+    return (img(), info, torch.from_numpy(gt), torch.tensor([G]), torch.ones(1),
+            img(), info.clone(), torch.ones(1, 5), torch.zeros(1, dtype=torch.long), torch.zeros(1))
+
+
+def time_cpu_steps(steps, H=600, W=1200):
+    """Mean seconds per full DAF step (fwd + bwd + clip + SGD) on the CPU."""
+    torch.manual_seed(0)
+    m = OracleDAF().train()
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = torch.optim.SGD(params, lr=2e-3, momentum=0.9, weight_decay=5e-4)
+    batch = synthetic_batch(H, W)
+    rng = np.random.RandomState(3)
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        loss = total_loss(m(batch, rng))
+        loss.backward()
+        tot = torch.sqrt(sum((p.grad.norm() ** 2 for p in params if p.grad is not None)))
+        scale = 10.0 / max(float(tot), 10.0)
+        for p in params:
+            if p.grad is not None:
+                p.grad.mul_(scale)
+        opt.step()
+        times.append(time.perf_counter() - t0)
+    return float(np.mean(times))

@@ -69,8 +69,17 @@ def roi_align_bwd(top_grad, rois, B, C, H, W, scale):
     per-tap contribution is rounded to float exactly as the atomicAdd argument is."""
     R, _, ah, aw = top_grad.shape
     bidx, hs, ws, hr, wr, hv, wv = _align_geometry(rois, ah, aw, scale, H, W)
-    acc = np.zeros((B, C, H, W), np.float64)
+    acc = np.zeros(B * C * H * W, np.float64)
     cidx = np.arange(C)[:, None, None]
+    idx_chunks, val_chunks = [], []
+
+    def flush():
+        if idx_chunks:
+            acc[:] += np.bincount(np.concatenate(idx_chunks), np.concatenate(val_chunks),
+                                  minlength=acc.size)
+            idx_chunks.clear()
+            val_chunks.clear()
+
     for r in range(R):
         valid = (hv[r][:, None] & wv[r][None, :])
         if not valid.any():
@@ -85,15 +94,18 @@ def roi_align_bwd(top_grad, rois, B, C, H, W, scale):
         c_ur = ((td.astype(f64) * (1.0 - h_r.astype(f64))) * w_r.astype(f64)).astype(f32)
         c_dl = ((td * h_r).astype(f32) * om).astype(f32)
         c_dr = ((td * h_r).astype(f32) * w_r).astype(f32)
-        a = acc[bidx[r]]
         m = np.broadcast_to(valid[None], td.shape)
-        cc = np.broadcast_to(cidx, td.shape)[m]
+        base = (bidx[r] * C + np.broadcast_to(cidx, td.shape)[m]) * H
         yy = np.broadcast_to(y[None], td.shape)[m]
         xx = np.broadcast_to(x[None], td.shape)[m]
-        np.add.at(a, (cc, yy, xx), c_ul[m])
-        np.add.at(a, (cc, yy, xx + 1), c_ur[m])
-        np.add.at(a, (cc, yy + 1, xx), c_dl[m])
-        np.add.at(a, (cc, yy + 1, xx + 1), c_dr[m])
+        ul = (base + yy) * W + xx
+        dl = (base + yy + 1) * W + xx
+        idx_chunks += [ul, ul + 1, dl, dl + 1]
+        val_chunks += [c_ul[m], c_ur[m], c_dl[m], c_dr[m]]
+        if len(idx_chunks) >= 128:
+            flush()
+    flush()
+    acc = acc.reshape(B, C, H, W)
     return acc.astype(np.float32)
 
 

@@ -118,6 +118,7 @@ class _fasterRCNN(nn.Module):
         self.RCNN_instanceDA = _InstanceDA(self.instance_dim)
         self.consistency_loss = nn.MSELoss(reduction="sum")
         self.replay_rng = None  # tests: np.random-like object -> reference-exact sampling
+        self.capture = None     # tests: dict receiving the proposal-layer rois
 
     # ------------------------------------------------------------------ pieces
     def _pool(self, feat, rois):
@@ -179,6 +180,8 @@ class _fasterRCNN(nn.Module):
                                                     num_boxes, rng=self.replay_rng)
         # target RPN in eval mode (faster_rcnn.py:140-142): TEST proposals, no losses
         tgt_rois = rpn.RPN_proposal((t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST"))
+        if self.capture is not None:
+            self.capture.update(s_rois=rois.detach().clone(), t_rois=tgt_rois.detach().clone())
 
         rois, rois_label, rois_target, rois_inside_ws, rois_outside_ws = \
             self.RCNN_proposal_target(rois, gt_boxes, num_boxes, rng=self.replay_rng)
