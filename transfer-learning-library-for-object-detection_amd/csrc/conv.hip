@@ -38,8 +38,13 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // ======================================================================= forward
 // Block tile: BM = WM*MI*32 output channels x BN = TH*32 pixels (TH = WN*NJ rows of 32).
+// K is consumed in chunks of CK input channels (KC = CK*KS*KS).  The 32x32x2 MFMA pairs
+// GEMM rows k and k + KC/2 (lanes 0-31 / 32-63): since KC/2 = (CK/2)*KS*KS, row k+KC/2 is
+// the same tap (kh,kw) CK/2 channels further, so every LDS operand read in the fully
+// unrolled chunk is a lane-constant base plus a compile-time immediate.
 template <int WM, int WN, int MI, int NJ, int CK, int KS>
 struct FwdCfg {
+  static_assert(CK % 2 == 0, "CK must be even (K pairing)");
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * MI * 32;
   static constexpr int TH = WN * NJ;
@@ -47,6 +52,7 @@ struct FwdCfg {
   static constexpr int PH = TH + KS - 1, PW = TW + KS - 1;
   static constexpr int KK = KS * KS;
   static constexpr int KC = CK * KK;              // GEMM K per chunk
+  static constexpr int HALF = KC / 2;
   static constexpr int A_ELEMS = KC * BM;         // As[KC][BM]
   static constexpr int B_ELEMS = CK * PH * PW;    // Bs[CK][PH][PW]
   static constexpr int A_V4 = A_ELEMS / 4;
@@ -62,10 +68,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     int tiles_w, int tiles_h) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* As0 = lds;
-  float* Bs0 = lds + C::A_ELEMS;
-  float* As1 = lds + C::A_ELEMS + C::B_ELEMS;
-  float* Bs1 = As1 + C::A_ELEMS;
 
   const int nwg = tiles_m * tiles_w * tiles_h * N;
   int t = xcd_remap(blockIdx.x, nwg);
@@ -83,6 +85,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
   const float* Xn = X + (size_t)n * Cin * H * W;
   const int nchunks = (Cin + CK - 1) / CK;
   const int Ktot = Cin * C::KK;
+  const bool vec4 = (Cout & 3) == 0;
+
+  // lane-constant operand bases (see header comment)
+  const int a_base = khalf * C::HALF * C::BM + wm * MI * 32 + l32;
+  const int b_base = khalf * (CK / 2) * C::PH * C::PW + wn * NJ * C::PW + l32;
 
   float4 ra[C::A_PER];
   float rb[C::B_PER];
@@ -98,7 +105,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
         const int k = k0 + kk, m = m0 + mm;
         if (k < Ktot && m < Cout) {
           const float* src = Wk + (size_t)k * Cout + m;
-          if ((Cout & 3) == 0) {
+          if (vec4) {
             v = *reinterpret_cast<const float4*>(src);
           } else {  // rows not 16-B aligned (e.g. dgrad of a 3-channel input)
             v.x = src[0];
@@ -146,30 +153,34 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   load_chunk(0);
-  store_chunk(As0, Bs0);
+  store_chunk(lds, lds + C::A_ELEMS);
   __syncthreads();
 
   for (int ch = 0; ch < nchunks; ++ch) {
-    float* As = (ch & 1) ? As1 : As0;
-    float* Bs = (ch & 1) ? Bs1 : Bs0;
+    const float* As = lds + (ch & 1) * (C::A_ELEMS + C::B_ELEMS);
+    const float* Bs = As + C::A_ELEMS;
+    const float* Al = As + a_base;
+    const float* Bl = Bs + b_base;
     const bool more = ch + 1 < nchunks;
     if (more) load_chunk(ch + 1);
-    const int kvalid = min(C::KC, (Cin - ch * CK) * C::KK);
-    for (int kk = 0; kk < kvalid; kk += 2) {
-      const int k = kk + khalf;
-      const int ci = k / C::KK, s = k % C::KK;
-      const int kh = s / KS, kw = s % KS;
+#pragma unroll
+    for (int kk = 0; kk < C::HALF; ++kk) {
+      const int ci = kk / C::KK, s = kk % C::KK;        // compile-time after unrolling
+      const int boff = (ci * C::PH + s / KS) * C::PW + s % KS;
       float a[MI], b[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = As[k * C::BM + wm * MI * 32 + i * 32 + l32];
+      for (int i = 0; i < MI; ++i) a[i] = Al[kk * C::BM + i * 32];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = Bs[(ci * C::PH + wn * NJ + j + kh) * C::PW + l32 + kw];
+      for (int j = 0; j < NJ; ++j) b[j] = Bl[boff + j * C::PW];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
     }
-    if (more) store_chunk((ch & 1) ? As0 : As1, (ch & 1) ? Bs0 : Bs1);
+    if (more) {
+      float* Ad = lds + ((ch + 1) & 1) * (C::A_ELEMS + C::B_ELEMS);
+      store_chunk(Ad, Ad + C::A_ELEMS);
+    }
     __syncthreads();
   }
 
@@ -197,7 +208,8 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
 
 // ======================================================================= wgrad
 // Block tile: BM = WM*MI*32 output channels x BN = WN*NJ*32 GEMM columns n=(ci,kh,kw);
-// K = pixels, chunked as TH=2 rows x 32 columns; grid.y = split-K slices.
+// K = pixels, chunked as TH=2 rows x 32 columns.  The MFMA pairs pixel (0, c) with
+// (1, c) (lanes 0-31 / 32-63): +1 row, a lane-constant offset.  grid.y = split-K slices.
 template <int WM, int WN, int MI, int NJ, int KS>
 struct WgCfg {
   static constexpr int NT = WM * WN * 64;
@@ -209,7 +221,7 @@ struct WgCfg {
   static constexpr int NCI = BN / KK + 2;           // channels a column tile can span
   static constexpr int GP = BM + 1;                  // padded pitch of Gs[p][m]
   static constexpr int G_ELEMS = P * GP;
-  static constexpr int X_ELEMS = NCI * PH * PW + 1;  // +1: a zero slot for dead columns
+  static constexpr int X_ELEMS = NCI * PH * PW + PW + 8;  // + a zero row for dead columns
   static constexpr int G_PER = (BM * P + NT - 1) / NT;
   static constexpr int X_PER = (NCI * PH * PW + NT - 1) / NT;
   static constexpr int LDS_FLOATS = 2 * (G_ELEMS + X_ELEMS);
@@ -221,10 +233,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
     int Cin, int H, int W, int Cout, int tiles_m, int tiles_n, int splits, int chunks_per_split) {
   using C = WgCfg<WM, WN, MI, NJ, KS>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* Gs0 = lds;
-  float* Xs0 = lds + C::G_ELEMS;
-  float* Gs1 = Xs0 + C::X_ELEMS;
-  float* Xs1 = Gs1 + C::G_ELEMS;
 
   const int nwg = tiles_m * tiles_n * splits;
   int t = xcd_remap(blockIdx.x, nwg);
@@ -245,18 +253,21 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
   const int c_begin = split * chunks_per_split;
   const int c_end = min(total_chunks, c_begin + chunks_per_split);
 
-  // per-lane B column offsets into Xs (dead columns read the zero slot)
+  // per-lane B column offsets into Xs (+1 patch row for the khalf=1 pixel row); dead
+  // columns read the zero row at the end of the patch
+  const int zero_row = C::NCI * C::PH * C::PW;
   int boff[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = n0 + wn * NJ * 32 + j * 32 + l32;
     if (col < Ktot) {
       const int ci = col / C::KK - cb, s = col % C::KK;
-      boff[j] = (ci * C::PH + s / KS) * C::PW + s % KS;
+      boff[j] = (ci * C::PH + s / KS + khalf) * C::PW + s % KS;
     } else {
-      boff[j] = -1;
+      boff[j] = zero_row;
     }
   }
+  const int a_base = khalf * C::TW * C::GP + wm * MI * 32 + l32;
 
   float rg[C::G_PER];
   float rx[C::X_PER];
@@ -314,37 +325,39 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (tid == 0) { Xs0[C::X_ELEMS - 1] = 0.f; Xs1[C::X_ELEMS - 1] = 0.f; }
-  int zslot[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) zslot[j] = boff[j] < 0;
-
+  constexpr int BUF = C::G_ELEMS + C::X_ELEMS;
+  for (int i = tid; i < C::X_ELEMS - zero_row; i += C::NT) {
+    lds[C::G_ELEMS + zero_row + i] = 0.f;
+    lds[BUF + C::G_ELEMS + zero_row + i] = 0.f;
+  }
   if (c_begin < c_end) {
     load_chunk(c_begin);
-    store_chunk(Gs0, Xs0);
+    store_chunk(lds, lds + C::G_ELEMS);
   }
   __syncthreads();
   for (int c = c_begin; c < c_end; ++c) {
     const int it = c - c_begin;
-    float* Gs = (it & 1) ? Gs1 : Gs0;
-    float* Xs = (it & 1) ? Xs1 : Xs0;
+    const float* Gs = lds + (it & 1) * BUF;
+    const float* Xs = Gs + C::G_ELEMS;
+    const float* Gl = Gs + a_base;
     const bool more = c + 1 < c_end;
     if (more) load_chunk(c + 1);
-#pragma unroll 4
-    for (int ks = 0; ks < C::P / 2; ++ks) {
-      const int p = 2 * ks + khalf;
-      const int pofs = (p / C::TW) * C::PW + (p % C::TW);
+#pragma unroll
+    for (int ks = 0; ks < C::TW; ++ks) {
       float a[MI], b[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = Gs[p * C::GP + wm * MI * 32 + i * 32 + l32];
+      for (int i = 0; i < MI; ++i) a[i] = Gl[ks * C::GP + i * 32];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = zslot[j] ? Xs[C::X_ELEMS - 1] : Xs[boff[j] + pofs];
+      for (int j = 0; j < NJ; ++j) b[j] = Xs[boff[j] + ks];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
     }
-    if (more) store_chunk((it & 1) ? Gs0 : Gs1, (it & 1) ? Xs0 : Xs1);
+    if (more) {
+      float* Gd = lds + ((it + 1) & 1) * BUF;
+      store_chunk(Gd, Gd + C::G_ELEMS);
+    }
     __syncthreads();
   }
 
@@ -470,12 +483,12 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
 static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias, float* Y, int N,
                              int Cin, int H, int W, int Cout, int KS, int relu, hipStream_t s) {
   if (KS == 3) {
-    if (Cout <= 64) return launch_fwd<1, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-    return launch_fwd<2, 2, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    if (Cout <= 64) return launch_fwd<1, 8, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd<2, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
   }
   if (KS == 1) {
-    if (Cout <= 64) return launch_fwd<1, 4, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-    return launch_fwd<2, 2, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    if (Cout <= 64) return launch_fwd<1, 8, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd<2, 4, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
   }
   set_error("conv: only 1x1 and 3x3 kernels (stride 1) are implemented");
   return kUnsupported;
@@ -504,9 +517,9 @@ static int launch_wgrad(const float* G, const float* X, float* slab, int splits,
 }
 
 int wgrad_splits(int N, int Cin, int H, int W, int Cout, int KS) {
-  const int tiles = div_up(Cout, 128) * div_up(Cin * KS * KS, 128);
+  const int tiles = div_up(Cout, 128) * div_up(Cin * KS * KS, 256);
   const int chunks = N * div_up(H, 2) * div_up(W, 32);
-  int splits = std::max(1, std::min(chunks / 8, div_up(1024, tiles)));
+  int splits = std::max(1, std::min(chunks / 8, div_up(512, tiles)));
   return std::min(splits, 64);
 }
 
@@ -565,7 +578,7 @@ extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, i
   }
   float* slab = static_cast<float*>(ws);
   int st;
-  if (KS == 3) st = launch_wgrad<2, 2, 2, 2, 3>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
+  if (KS == 3) st = launch_wgrad<2, 4, 2, 2, 3>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
   else if (KS == 1) st = launch_wgrad<2, 2, 2, 2, 1>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
   else { set_error("conv wgrad: only 1x1 and 3x3"); return kUnsupported; }
   if (st) return st;
