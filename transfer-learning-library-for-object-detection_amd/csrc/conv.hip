@@ -24,6 +24,11 @@ namespace tlod {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Out-of-range staging loads read this zero block instead of branching (a branch per
+// load makes hipcc wait vmcnt(0) after each one; a select after the load pins the wait
+// to the load instead of the LDS store that follows the MFMA phase).
+__device__ __attribute__((aligned(16))) float g_zero[16];
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -58,10 +63,10 @@ struct FwdCfg {
   static constexpr int A_V4 = A_ELEMS / 4;
   static constexpr int A_PER = (A_V4 + NT - 1) / NT;
   static constexpr int B_PER = (B_ELEMS + NT - 1) / NT;
-  static constexpr int LDS_FLOATS = 2 * (A_ELEMS + B_ELEMS);
+  static constexpr int LDS_FLOATS = 2 * (A_ELEMS + B_ELEMS) + BM;  // + bias tile
 };
 
-template <int WM, int WN, int MI, int NJ, int CK, int KS>
+template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
 __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ Wk, const float* __restrict__ bias,
     float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int relu, int tiles_m,
@@ -85,7 +90,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
   const float* Xn = X + (size_t)n * Cin * H * W;
   const int nchunks = (Cin + CK - 1) / CK;
   const int Ktot = Cin * C::KK;
-  const bool vec4 = (Cout & 3) == 0;
 
   // lane-constant operand bases (see header comment)
   const int a_base = khalf * C::HALF * C::BM + wm * MI * 32 + l32;
@@ -94,26 +98,25 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
   float4 ra[C::A_PER];
   float rb[C::B_PER];
 
+  // All staging loads are unconditional (out-of-range lanes read a clamped, valid
+  // address and select 0): a branch per load makes hipcc wait vmcnt(0) after each one.
   auto load_chunk = [&](int ch) {
     const int k0 = ch * C::KC;
 #pragma unroll
     for (int i = 0; i < C::A_PER; ++i) {
       const int e = tid + i * C::NT;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < C::A_V4) {
-        const int kk = e / (C::BM / 4), mm = (e % (C::BM / 4)) * 4;
-        const int k = k0 + kk, m = m0 + mm;
-        if (k < Ktot && m < Cout) {
-          const float* src = Wk + (size_t)k * Cout + m;
-          if (vec4) {
-            v = *reinterpret_cast<const float4*>(src);
-          } else {  // rows not 16-B aligned (e.g. dgrad of a 3-channel input)
-            v.x = src[0];
-            v.y = m + 1 < Cout ? src[1] : 0.f;
-            v.z = m + 2 < Cout ? src[2] : 0.f;
-            v.w = m + 3 < Cout ? src[3] : 0.f;
-          }
-        }
+      const int kk = e / (C::BM / 4), mm = (e % (C::BM / 4)) * 4;
+      const int k = k0 + kk, m = m0 + mm;
+      const bool ok = (e < C::A_V4) && (k < Ktot) && (m < Cout);
+      const float* src = ok ? Wk + (size_t)k * Cout + m : g_zero;
+      float4 v;
+      if constexpr (VEC4) {
+        v = *reinterpret_cast<const float4*>(src);
+      } else {  // rows not 16-B aligned (e.g. dgrad of a 3-channel input)
+        v.x = src[0];
+        v.y = *((ok && m + 1 < Cout) ? src + 1 : g_zero);
+        v.z = *((ok && m + 2 < Cout) ? src + 2 : g_zero);
+        v.w = *((ok && m + 3 < Cout) ? src + 3 : g_zero);
       }
       ra[i] = v;
     }
@@ -121,14 +124,10 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < C::B_PER; ++i) {
       const int e = tid + i * C::NT;
-      float v = 0.f;
-      if (e < C::B_ELEMS) {
-        const int ci = e / (C::PH * C::PW), r = (e / C::PW) % C::PH, c = e % C::PW;
-        const int gh = h0 - pad + r, gw = w0 - pad + c, gc = ci0 + ci;
-        if (gc < Cin && gh >= 0 && gh < H && gw >= 0 && gw < W)
-          v = Xn[((size_t)gc * H + gh) * W + gw];
-      }
-      rb[i] = v;
+      const int ci = e / (C::PH * C::PW), r = (e / C::PW) % C::PH, c = e % C::PW;
+      const int gh = h0 - pad + r, gw = w0 - pad + c, gc = ci0 + ci;
+      const bool ok = (e < C::B_ELEMS) && gc < Cin && gh >= 0 && gh < H && gw >= 0 && gw < W;
+      rb[i] = *(ok ? Xn + ((size_t)gc * H + gh) * W + gw : g_zero);
     }
   };
   auto store_chunk = [&](float* As, float* Bs) {
@@ -152,6 +151,12 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  float* bias_s = lds + 2 * (C::A_ELEMS + C::B_ELEMS);
+  if (tid < C::BM) {
+    const int co = m0 + tid;
+    const float bv = bias ? bias[co < Cout ? co : 0] : 0.f;
+    bias_s[tid] = (bias && co < Cout) ? bv : 0.f;
+  }
   load_chunk(0);
   store_chunk(lds, lds + C::A_ELEMS);
   __syncthreads();
@@ -195,10 +200,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
       if (h >= H || w >= W) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int co = m0 + ml;
         if (co < Cout) {
           float v = acc[i][j][r];
-          if (bias) v += bias[co];
+          if (bias) v += bias_s[ml];
           if (relu) v = fmaxf(v, 0.f);
           Yn[((size_t)co * H + h) * W + w] = v;
         }
@@ -277,28 +283,23 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
     const int h0 = chi * C::TH, w0 = cwi * C::TW;
     const float* Gn = G + (size_t)n * Cout * H * W;
     const float* Xn = X + (size_t)n * Cin * H * W;
+    // unconditional loads from clamped addresses (see conv_fwd_kernel)
 #pragma unroll
     for (int i = 0; i < C::G_PER; ++i) {
       const int e = tid + i * C::NT;  // e -> (m, p), p fastest: 128-B row segments
-      float v = 0.f;
-      if (e < C::BM * C::P) {
-        const int m = e / C::P, p = e % C::P;
-        const int h = h0 + p / C::TW, w = w0 + p % C::TW;
-        if (m0 + m < Cout && h < H && w < W) v = Gn[((size_t)(m0 + m) * H + h) * W + w];
-      }
-      rg[i] = v;
+      const int m = e / C::P, p = e % C::P;
+      const int h = h0 + p / C::TW, w = w0 + p % C::TW;
+      const bool ok = (e < C::BM * C::P) && (m0 + m < Cout) && h < H && w < W;
+      rg[i] = *(ok ? Gn + ((size_t)(m0 + m) * H + h) * W + w : g_zero);
     }
 #pragma unroll
     for (int i = 0; i < C::X_PER; ++i) {
       const int e = tid + i * C::NT;
-      float v = 0.f;
-      if (e < C::NCI * C::PH * C::PW) {
-        const int ci = e / (C::PH * C::PW), rr = (e / C::PW) % C::PH, cc = e % C::PW;
-        const int gc = cb + ci, gh = h0 - pad + rr, gw = w0 - pad + cc;
-        if (gc < Cin && gh >= 0 && gh < H && gw >= 0 && gw < W)
-          v = Xn[((size_t)gc * H + gh) * W + gw];
-      }
-      rx[i] = v;
+      const int ci = e / (C::PH * C::PW), rr = (e / C::PW) % C::PH, cc = e % C::PW;
+      const int gc = cb + ci, gh = h0 - pad + rr, gw = w0 - pad + cc;
+      const bool ok = (e < C::NCI * C::PH * C::PW) && gc < Cin && gh >= 0 && gh < H && gw >= 0 &&
+                      gw < W;
+      rx[i] = *(ok ? Xn + ((size_t)gc * H + gh) * W + gw : g_zero);
     }
   };
   auto store_chunk = [&](float* Gs, float* Xs) {
@@ -460,7 +461,7 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
 }
 
 // ======================================================================= launchers
-template <int WM, int WN, int MI, int NJ, int CK, int KS>
+template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
 static int launch_fwd(const float* X, const float* Wk, const float* bias, float* Y, int N,
                       int Cin, int H, int W, int Cout, int relu, hipStream_t s) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
@@ -468,7 +469,7 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
   const long long nwg = (long long)tiles_m * tiles_w * tiles_h * N;
   TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
   const size_t lds = C::LDS_FLOATS * sizeof(float);
-  auto kern = conv_fwd_kernel<WM, WN, MI, NJ, CK, KS>;
+  auto kern = conv_fwd_kernel<WM, WN, MI, NJ, CK, KS, VEC4>;
   static bool attr = false;
   if (!attr) {
     TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -480,15 +481,23 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
   return kOk;
 }
 
+template <int WM, int WN, int MI, int NJ, int CK, int KS>
+static int launch_fwd_v(const float* X, const float* Wk, const float* bias, float* Y, int N,
+                        int Cin, int H, int W, int Cout, int relu, hipStream_t s) {
+  if ((Cout & 3) == 0)
+    return launch_fwd<WM, WN, MI, NJ, CK, KS, true>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+  return launch_fwd<WM, WN, MI, NJ, CK, KS, false>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+}
+
 static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias, float* Y, int N,
                              int Cin, int H, int W, int Cout, int KS, int relu, hipStream_t s) {
   if (KS == 3) {
-    if (Cout <= 64) return launch_fwd<1, 8, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-    return launch_fwd<2, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    if (Cout <= 64) return launch_fwd_v<1, 8, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd_v<2, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
   }
   if (KS == 1) {
-    if (Cout <= 64) return launch_fwd<1, 8, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-    return launch_fwd<2, 4, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    if (Cout <= 64) return launch_fwd_v<1, 8, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd_v<2, 4, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
   }
   set_error("conv: only 1x1 and 3x3 kernels (stride 1) are implemented");
   return kUnsupported;
