@@ -1,0 +1,77 @@
+"""tlod.dist.GradBucketReducer on CPU with the gloo backend, world_size 2: gradients
+after finish() equal the average of the per-rank gradients (the DataParallel loss.mean()
+semantics, methods/DAF/DAF_train.py:341-342 / :397), weights are broadcast from rank 0,
+and buckets launch from the post-accumulate hooks in any completion order."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(seed):
+    torch.manual_seed(seed)
+    m = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 48),
+                            torch.nn.ReLU(), torch.nn.Linear(48, 5))
+    m[0].bias.requires_grad_(False)  # a frozen parameter must not break bucketing
+    return m
+
+
+def _data(rank):
+    g = torch.Generator().manual_seed(100 + rank)
+    return torch.randn(16, 32, generator=g), torch.randn(16, 5, generator=g)
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "transfer-learning-library-for-object-detection_amd"))
+    from tlod.dist import GradBucketReducer, init_from_env
+    init_from_env(backend="gloo")
+    m = _model(seed=rank)  # different init per rank: the reducer must broadcast rank 0's
+    red = GradBucketReducer(m, bucket_mb=0.004)  # ~1000 floats -> several buckets
+    assert len(red.buckets) >= 3
+    for step in range(2):
+        red.zero_grad()
+        x, y = _data(rank * 10 + step)
+        loss = ((m(x) - y) ** 2).mean()
+        loss.backward()
+        red.finish()
+        if step == 1:
+            out[rank] = {k: p.grad.clone() for k, p in m.named_parameters() if p.requires_grad}
+            out[f"w{rank}"] = {k: p.detach().clone() for k, p in m.named_parameters()}
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_reducer_gloo_world2():
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    # reference: rank-0 weights, average of the two ranks' step-1 gradients
+    m = _model(seed=0)
+    grads = []
+    for rank in range(2):
+        m.zero_grad()
+        x, y = _data(rank * 10 + 1)
+        ((m(x) - y) ** 2).mean().backward()
+        grads.append({k: p.grad.clone() for k, p in m.named_parameters() if p.requires_grad})
+    for k in grads[0]:
+        ref = (grads[0][k] + grads[1][k]) / 2
+        torch.testing.assert_close(out[0][k], ref, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(out[1][k], out[0][k], rtol=0, atol=0)
+    for k in out["w0"]:
+        assert torch.equal(out["w0"][k], out["w1"][k])
