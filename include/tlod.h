@@ -194,16 +194,22 @@ int tlod_proposal_target_f32(const float* rois, int B, int R, const float* gt_bo
  * dgrad: dx = conv_transpose(dy, weight)                            dx (N,Cin,H,W)
  * wgrad: dw (+)= sum_n,p dy (x) x-patches, deterministic split-K    dw (Cout,Cin,KS,KS)
  *        (accumulate != 0 adds into dw, like autograd grad accumulation)
+ * fwd/dgrad split the input channels over workgroups (deterministic slab reduction) when
+ * the output tiles cannot fill the chip; *_workspace_bytes reports the slab size (0 when no
+ * split is used).
  * relu_bwd_bias: g = dy * (y > 0) (y may be NULL: g = dy), db += sum over n,h,w of g
  *        (db may be NULL).  g may alias dy. */
 int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
                            tlod_stream_t stream);
 int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, int KS, float* wd,
                              tlod_stream_t stream);
+size_t tlod_conv_fwd_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS);
+size_t tlod_conv_dgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS);
 int tlod_conv_fwd_f32(const float* x, const float* wk, const float* bias, float* y, int N,
-                      int Cin, int H, int W, int Cout, int KS, int relu, tlod_stream_t stream);
+                      int Cin, int H, int W, int Cout, int KS, int relu, void* ws,
+                      size_t ws_bytes, tlod_stream_t stream);
 int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, int N, int Cin, int H,
-                        int W, int Cout, int KS, tlod_stream_t stream);
+                        int W, int Cout, int KS, void* ws, size_t ws_bytes, tlod_stream_t stream);
 size_t tlod_conv_wgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS);
 int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, int accumulate, int N,
                         int Cin, int H, int W, int Cout, int KS, void* ws, size_t ws_bytes,

@@ -69,3 +69,23 @@ def test_wgrad_deterministic():
     a = conv_wgrad(g, x, 3)
     b = conv_wgrad(g, x, 3)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 512, 512, 37, 75), (1, 512, 512, 12, 20),
+                                            (2, 256, 512, 38, 40)])
+def test_conv_split_k_paths(N, Cin, Cout, H, W):
+    """Small spatial maps take the split-K path (slab + deterministic reduce)."""
+    from tlod import _lib
+    from tlod.conv import conv_dgrad, conv_fwd
+    assert _lib.lib().tlod_conv_fwd_workspace_bytes(N, Cin, H, W, Cout, 3) > 0
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    y = conv_fwd(x.to(dev), w.to(dev), b.to(dev), relu=True)
+    _close(y, F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1)))
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    dx = conv_dgrad(gy.to(dev), w.to(dev))
+    _close(dx, torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=1))
+    y2 = conv_fwd(x.to(dev), w.to(dev), b.to(dev), relu=True)
+    assert torch.equal(y, y2)  # deterministic

@@ -70,16 +70,17 @@ template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
 __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ Wk, const float* __restrict__ bias,
     float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int relu, int tiles_m,
-    int tiles_w, int tiles_h) {
+    int tiles_w, int tiles_h, int ksplit, int cps, float* __restrict__ slab) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 
-  const int nwg = tiles_m * tiles_w * tiles_h * N;
+  const int nwg = tiles_m * tiles_w * tiles_h * N * ksplit;
   int t = xcd_remap(blockIdx.x, nwg);
   const int mt = t % tiles_m; t /= tiles_m;
   const int tw = t % tiles_w; t /= tiles_w;
-  const int th = t % tiles_h;
-  const int n = t / tiles_h;
+  const int th = t % tiles_h; t /= tiles_h;
+  const int n = t % N;
+  const int split = t / N;  // split-K slice over input-channel chunks
   const int m0 = mt * C::BM, w0 = tw * C::TW, h0 = th * C::TH;
   const int pad = KS / 2;
 
@@ -157,16 +158,20 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     const float bv = bias ? bias[co < Cout ? co : 0] : 0.f;
     bias_s[tid] = (bias && co < Cout) ? bv : 0.f;
   }
-  load_chunk(0);
-  store_chunk(lds, lds + C::A_ELEMS);
+  const int c_begin = split * cps, c_end = min(nchunks, c_begin + cps);
+  if (c_begin < c_end) {
+    load_chunk(c_begin);
+    store_chunk(lds, lds + C::A_ELEMS);
+  }
   __syncthreads();
 
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const float* As = lds + (ch & 1) * (C::A_ELEMS + C::B_ELEMS);
+  for (int ch = c_begin; ch < c_end; ++ch) {
+    const int it = ch - c_begin;
+    const float* As = lds + (it & 1) * (C::A_ELEMS + C::B_ELEMS);
     const float* Bs = As + C::A_ELEMS;
     const float* Al = As + a_base;
     const float* Bl = Bs + b_base;
-    const bool more = ch + 1 < nchunks;
+    const bool more = ch + 1 < c_end;
     if (more) load_chunk(ch + 1);
 #pragma unroll
     for (int kk = 0; kk < C::HALF; ++kk) {
@@ -183,14 +188,17 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
         for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
     }
     if (more) {
-      float* Ad = lds + ((ch + 1) & 1) * (C::A_ELEMS + C::B_ELEMS);
+      float* Ad = lds + ((it + 1) & 1) * (C::A_ELEMS + C::B_ELEMS);
       store_chunk(Ad, Ad + C::A_ELEMS);
     }
     __syncthreads();
   }
 
-  // epilogue: lane owns pixel column l32; rows (co) = (r&3) + 8*(r>>2) + 4*khalf
-  float* Yn = Y + (size_t)n * Cout * H * W;
+  // epilogue: lane owns pixel column l32; rows (co) = (r&3) + 8*(r>>2) + 4*khalf.
+  // Split-K: raw partial sums go to slab[split] (bias/ReLU applied by the reduce).
+  float* Yn = (ksplit > 1 ? slab + (size_t)split * N * Cout * H * W : Y) + (size_t)n * Cout * H * W;
+  if (ksplit > 1) relu = 0;
+  const bool add_bias = bias && ksplit == 1;
   const int w = w0 + l32;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -204,7 +212,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
         const int co = m0 + ml;
         if (co < Cout) {
           float v = acc[i][j][r];
-          if (bias) v += bias_s[ml];
+          if (add_bias) v += bias_s[ml];
           if (relu) v = fmaxf(v, 0.f);
           Yn[((size_t)co * H + h) * W + w] = v;
         }
@@ -393,6 +401,20 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
   }
 }
 
+// y = act(sum_s slab[s] + bias), summed in split order (deterministic).
+__global__ void fwd_split_reduce_kernel(const float* __restrict__ slab, int ksplit, size_t count,
+                                        const float* __restrict__ bias, int Cout, int HW,
+                                        int relu, float* __restrict__ y) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float v = slab[i];
+    for (int k = 1; k < ksplit; ++k) v += slab[(size_t)k * count + i];
+    if (bias) v += bias[(i / HW) % Cout];
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = v;
+  }
+}
+
 // ======================================================================= helpers
 // Wk[(ci*KK + s)][co] = W[co][ci][s]   (forward operand, K-major)
 __global__ void pack_fwd_kernel(const float* __restrict__ Wt, float* __restrict__ Wk, int Cout,
@@ -461,13 +483,39 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
 }
 
 // ======================================================================= launchers
+struct FwdPlan { int tiles_m, tiles_w, tiles_h, ksplit, cps; };
+
+template <int WM, int WN, int MI, int NJ, int CK, int KS>
+static FwdPlan plan_fwd(int N, int Cin, int H, int W, int Cout) {
+  using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
+  FwdPlan p;
+  p.tiles_m = div_up(Cout, C::BM);
+  p.tiles_w = div_up(W, C::TW);
+  p.tiles_h = div_up(H, C::TH);
+  const int nchunks = div_up(Cin, CK);
+  const long long base = (long long)p.tiles_m * p.tiles_w * p.tiles_h * N;
+  // split K over input-channel chunks when the output tiles alone cannot fill ~3 waves
+  // of workgroups on the 256 CUs (conv5 / RPN at 37x75: 120 tiles)
+  int ks = 1;
+  if (base < 512) ks = (int)std::min<long long>(std::min(8, std::max(1, nchunks / 4)), div_up(768, (int)base));
+  p.cps = div_up(nchunks, ks);
+  p.ksplit = div_up(nchunks, p.cps);
+  return p;
+}
+
 template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
 static int launch_fwd(const float* X, const float* Wk, const float* bias, float* Y, int N,
-                      int Cin, int H, int W, int Cout, int relu, hipStream_t s) {
+                      int Cin, int H, int W, int Cout, int relu, float* slab, size_t slab_bytes,
+                      hipStream_t s) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
-  const int tiles_m = div_up(Cout, C::BM), tiles_w = div_up(W, C::TW), tiles_h = div_up(H, C::TH);
-  const long long nwg = (long long)tiles_m * tiles_w * tiles_h * N;
+  const FwdPlan p = plan_fwd<WM, WN, MI, NJ, CK, KS>(N, Cin, H, W, Cout);
+  const long long nwg = (long long)p.tiles_m * p.tiles_w * p.tiles_h * N * p.ksplit;
   TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
+  const size_t out_elems = (size_t)N * Cout * H * W;
+  if (p.ksplit > 1 && slab_bytes < p.ksplit * out_elems * sizeof(float)) {
+    set_error("tlod_conv: workspace too small for split-K");
+    return kWorkspace;
+  }
   const size_t lds = C::LDS_FLOATS * sizeof(float);
   auto kern = conv_fwd_kernel<WM, WN, MI, NJ, CK, KS, VEC4>;
   static bool attr = false;
@@ -476,29 +524,50 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
     attr = true;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wk, bias, Y, N, Cin, H, W,
-                     Cout, relu, tiles_m, tiles_w, tiles_h);
+                     Cout, relu, p.tiles_m, p.tiles_w, p.tiles_h, p.ksplit, p.cps, slab);
   TLOD_LAUNCH_CHECK();
+  if (p.ksplit > 1) {
+    const int blocks = (int)std::min<size_t>((out_elems + 255) / 256, 4096);
+    hipLaunchKernelGGL(fwd_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, p.ksplit,
+                       out_elems, bias, Cout, H * W, relu, Y);
+    TLOD_LAUNCH_CHECK();
+  }
   return kOk;
 }
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS>
 static int launch_fwd_v(const float* X, const float* Wk, const float* bias, float* Y, int N,
-                        int Cin, int H, int W, int Cout, int relu, hipStream_t s) {
+                        int Cin, int H, int W, int Cout, int relu, float* slab, size_t sb,
+                        hipStream_t s) {
   if ((Cout & 3) == 0)
-    return launch_fwd<WM, WN, MI, NJ, CK, KS, true>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-  return launch_fwd<WM, WN, MI, NJ, CK, KS, false>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    return launch_fwd<WM, WN, MI, NJ, CK, KS, true>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, slab, sb, s);
+  return launch_fwd<WM, WN, MI, NJ, CK, KS, false>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, slab, sb, s);
 }
 
+// Dispatch on (KS, Cout): the tile configs used by the backbone.  ws_query != nullptr:
+// only report the split-K slab bytes the call would need.
 static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias, float* Y, int N,
-                             int Cin, int H, int W, int Cout, int KS, int relu, hipStream_t s) {
+                             int Cin, int H, int W, int Cout, int KS, int relu, float* slab,
+                             size_t sb, hipStream_t s, size_t* ws_query = nullptr) {
+#define TLOD_FWD_CFG(WM_, WN_, MI_, NJ_, CK_, KS_)                                              \
+  do {                                                                                          \
+    if (ws_query) {                                                                             \
+      const FwdPlan p = plan_fwd<WM_, WN_, MI_, NJ_, CK_, KS_>(N, Cin, H, W, Cout);             \
+      *ws_query = p.ksplit > 1 ? (size_t)p.ksplit * N * Cout * H * W * sizeof(float) : 0;       \
+      return kOk;                                                                               \
+    }                                                                                           \
+    return launch_fwd_v<WM_, WN_, MI_, NJ_, CK_, KS_>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, \
+                                                       slab, sb, s);                            \
+  } while (0)
   if (KS == 3) {
-    if (Cout <= 64) return launch_fwd_v<1, 8, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-    return launch_fwd_v<2, 4, 2, 2, 8, 3>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    if (Cout <= 64) TLOD_FWD_CFG(1, 8, 2, 2, 8, 3);
+    TLOD_FWD_CFG(2, 4, 2, 2, 8, 3);
   }
   if (KS == 1) {
-    if (Cout <= 64) return launch_fwd_v<1, 8, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
-    return launch_fwd_v<2, 4, 2, 2, 32, 1>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, s);
+    if (Cout <= 64) TLOD_FWD_CFG(1, 8, 2, 2, 32, 1);
+    TLOD_FWD_CFG(2, 4, 2, 2, 32, 1);
   }
+#undef TLOD_FWD_CFG
   set_error("conv: only 1x1 and 3x3 kernels (stride 1) are implemented");
   return kUnsupported;
 }
@@ -556,18 +625,32 @@ extern "C" int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, 
   return kOk;
 }
 
+extern "C" size_t tlod_conv_fwd_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS) {
+  size_t b = 0;
+  conv_fwd_dispatch(nullptr, nullptr, nullptr, nullptr, N, Cin, H, W, Cout, KS, 0, nullptr, 0,
+                    nullptr, &b);
+  return b;
+}
+
+extern "C" size_t tlod_conv_dgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS) {
+  return tlod_conv_fwd_workspace_bytes(N, Cout, H, W, Cin, KS);
+}
+
 extern "C" int tlod_conv_fwd_f32(const float* x, const float* wk, const float* bias, float* y,
                                  int N, int Cin, int H, int W, int Cout, int KS, int relu,
-                                 tlod_stream_t stream) {
+                                 void* ws, size_t ws_bytes, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
-  return conv_fwd_dispatch(x, wk, bias, y, N, Cin, H, W, Cout, KS, relu, (hipStream_t)stream);
+  return conv_fwd_dispatch(x, wk, bias, y, N, Cin, H, W, Cout, KS, relu, (float*)ws, ws_bytes,
+                           (hipStream_t)stream);
 }
 
 extern "C" int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, int N, int Cin,
-                                   int H, int W, int Cout, int KS, tlod_stream_t stream) {
+                                   int H, int W, int Cout, int KS, void* ws, size_t ws_bytes,
+                                   tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
   // dx[n, ci] = sum_{co, s'} Wd[(co, s')][ci] * dy[n, co, p + s' - pad]: forward form
-  return conv_fwd_dispatch(dy, wd, nullptr, dx, N, Cout, H, W, Cin, KS, 0, (hipStream_t)stream);
+  return conv_fwd_dispatch(dy, wd, nullptr, dx, N, Cout, H, W, Cin, KS, 0, (float*)ws, ws_bytes,
+                           (hipStream_t)stream);
 }
 
 extern "C" size_t tlod_conv_wgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS) {

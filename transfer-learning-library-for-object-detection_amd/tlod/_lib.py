@@ -71,8 +71,12 @@ SIGNATURES = {
                                          c_uint64, P, P, P, P, P, P, P, c_size_t, P]),
     "tlod_conv_pack_fwd_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
     "tlod_conv_pack_dgrad_f32": (c_int, [P, c_int, c_int, c_int, P, P]),
-    "tlod_conv_fwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
-    "tlod_conv_dgrad_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "tlod_conv_fwd_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "tlod_conv_dgrad_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "tlod_conv_fwd_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                                  c_size_t, P]),
+    "tlod_conv_dgrad_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t,
+                                    P]),
     "tlod_conv_wgrad_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "tlod_conv_wgrad_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                     c_size_t, P]),

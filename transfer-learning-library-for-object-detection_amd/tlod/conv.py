@@ -67,9 +67,11 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None):
     wk = pack_fwd(weight) if wk is None else wk
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
+    L = _lib.lib()
+    ws = _lib.workspace(L.tlod_conv_fwd_workspace_bytes(N, Cin, H, W, Cout, KS), x.device, "conv")
     _timed("fwd", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
-        _lib.lib().tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N, Cin, H,
-                                     W, Cout, KS, int(relu), _lib.stream_of(x)), "conv_fwd"))
+        L.tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N, Cin, H, W, Cout,
+                            KS, int(relu), _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv_fwd"))
     return y
 
 
@@ -79,9 +81,11 @@ def conv_dgrad(g, weight, wd=None):
     _, Cin, KS, _ = weight.shape
     wd = pack_dgrad(weight) if wd is None else wd
     dx = torch.empty((N, Cin, H, W), dtype=torch.float32, device=g.device)
+    L = _lib.lib()
+    ws = _lib.workspace(L.tlod_conv_dgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "conv")
     _timed("dgrad", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
-        _lib.lib().tlod_conv_dgrad_f32(_lib.ptr(g), _lib.ptr(wd), _lib.ptr(dx), N, Cin, H, W, Cout,
-                                       KS, _lib.stream_of(g)), "conv_dgrad"))
+        L.tlod_conv_dgrad_f32(_lib.ptr(g), _lib.ptr(wd), _lib.ptr(dx), N, Cin, H, W, Cout, KS,
+                              _lib.ptr(ws), ws.numel(), _lib.stream_of(g)), "conv_dgrad"))
     return dx
 
 
