@@ -71,9 +71,14 @@ int tlod_roi_align_bwd_f32(const float* top_grad, int B, int C, int H, int W,
 int tlod_roi_align_avg_fwd_f32(const float* feat, int B, int C, int H, int W,
                                const float* rois, int R, int ph, int pw, float scale,
                                float* out, tlod_stream_t stream);
+/* avg backward: with a workspace (tlod_roi_align_avg_bwd_workspace_bytes) the atomics go
+ * to a (B,H,W,C) accumulator (lanes over channels: contiguous atomics) that is then added
+ * into bottom_grad; ws == NULL accumulates straight into NCHW. */
+size_t tlod_roi_align_avg_bwd_workspace_bytes(int B, int C, int H, int W);
 int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W,
                                const float* rois, int R, int ph, int pw, float scale,
-                               float* bottom_grad, tlod_stream_t stream);
+                               float* bottom_grad, void* ws, size_t ws_bytes,
+                               tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ RoIPool
  * Replaces: roi_pooling_forward_cuda / roi_pooling_backward_cuda
@@ -216,6 +221,27 @@ int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, int accumula
                         tlod_stream_t stream);
 int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db, int N, int C,
                            int HW, tlod_stream_t stream);
+
+
+/* ------------------------------------------------------------------ Optimiser step
+ * Replaces: clip_gradient(model, 10.) lib/model/utils/net_utils.py:38-49 (per-param norm
+ *   loop + .item() host sync) + torch.optim.SGD(momentum) methods/DAF/DAF_train.py:323,408.
+ * chunks: device array of n_chunks descriptors (each <= 65536 elements of one tensor);
+ * per element: g' = g * clip/max(||G||, clip); d = g' + wd*p; buf = m*buf + d; p -= lr*buf
+ * (torch SGD semantics, dampening 0; buf starts at 0, so step 1 gives buf = d).
+ * clip_norm <= 0 disables clipping.  partials: float[n_chunks] scratch.  norm_scale: 2
+ * device floats receiving (total grad norm, applied scale).  Deterministic. */
+typedef struct tlod_sgd_chunk {
+  float* param;
+  const float* grad;
+  float* momentum_buf;
+  long long count;
+  float lr;
+  float weight_decay;
+} tlod_sgd_chunk;
+
+int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float momentum,
+                      float clip_norm, float* partials, float* norm_scale, tlod_stream_t stream);
 
 #ifdef __cplusplus
 }

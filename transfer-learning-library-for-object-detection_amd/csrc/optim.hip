@@ -1,0 +1,82 @@
+// Fused clip_gradient + SGD(momentum) over all trainable parameters.
+//
+// Replaces clip_gradient (lib/model/utils/net_utils.py:38-49: a Python loop of per-param
+// .norm() and a .item() host sync, then a second loop of p.grad.mul_) followed by
+// torch.optim.SGD (methods/DAF/DAF_train.py:406-408).  Three stream-ordered launches, no
+// host sync, deterministic (fixed-order reductions):
+//   1. per-chunk sum of squares of the gradients;
+//   2. one workgroup: total = sqrt(sum), scale = clip / max(total, clip);
+//   3. per chunk: g' = scale*g; d = g' + wd*p; buf = m*buf + d; p -= lr*buf.
+// HBM traffic: read g twice, read+write p and buf once: 6 x 4 B per parameter.
+#include "common.h"
+#include "tlod.h"
+
+namespace tlod {
+
+__global__ void __launch_bounds__(256) sgd_sumsq_kernel(const tlod_sgd_chunk* __restrict__ chunks,
+                                                        float* __restrict__ partials) {
+  const tlod_sgd_chunk c = chunks[blockIdx.x];
+  float s = 0.f;
+  for (long long i = threadIdx.x; i < c.count; i += 256) {
+    const float g = c.grad[i];
+    s += g * g;
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+  __shared__ float ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+}
+
+__global__ void __launch_bounds__(256) sgd_norm_kernel(const float* __restrict__ partials, int n,
+                                                       float clip, float* __restrict__ out) {
+  __shared__ double ws[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += (double)partials[i];
+  ws[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) ws[threadIdx.x] += ws[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float total = (float)sqrt(ws[0]);
+    out[0] = total;
+    out[1] = clip > 0.f ? clip / fmaxf(total, clip) : 1.f;  // net_utils.py:46
+  }
+}
+
+__global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* __restrict__ chunks,
+                                                         const float* __restrict__ norm_scale,
+                                                         float momentum) {
+  const tlod_sgd_chunk c = chunks[blockIdx.x];
+  const float scale = norm_scale[1];
+  for (long long i = threadIdx.x; i < c.count; i += 256) {
+    const float g = c.grad[i] * scale;
+    const float p = c.param[i];
+    const float d = g + c.weight_decay * p;
+    const float b = momentum * c.momentum_buf[i] + d;
+    c.momentum_buf[i] = b;
+    c.param[i] = p - c.lr * b;
+  }
+}
+
+}  // namespace tlod
+
+using namespace tlod;
+
+extern "C" int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float momentum,
+                                 float clip_norm, float* partials, float* norm_scale,
+                                 tlod_stream_t stream) {
+  TLOD_CHECK_ARG(n_chunks > 0 && chunks && partials && norm_scale, "bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sgd_sumsq_kernel, dim3(n_chunks), dim3(256), 0, s, chunks, partials);
+  TLOD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sgd_norm_kernel, dim3(1), dim3(256), 0, s, partials, n_chunks, clip_norm,
+                     norm_scale);
+  TLOD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sgd_update_kernel, dim3(n_chunks), dim3(256), 0, s, chunks, norm_scale,
+                     momentum);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}

@@ -182,6 +182,77 @@ __global__ void __launch_bounds__(kAvgThreads) roi_align_avg_bwd_kernel(
   }
 }
 
+// ------------------------------------------------------------ RoIAlignAvg backward, NHWC
+// One thread per channel, one workgroup per (roi, 256 channels): every atomic
+// wave-instruction adds 64 consecutive channels of one feature cell = 256 contiguous
+// bytes of the (B,H,W,C) accumulator — the shape the memory-side atomic unit runs at
+// full rate (one lane per row, the NCHW shape, runs ~17x slower).
+constexpr int kNhwcThreads = 256;
+
+__global__ void __launch_bounds__(kNhwcThreads) roi_align_avg_bwd_nhwc_kernel(
+    const float* __restrict__ top, float scale, int C, int H, int W, int ph, int pw,
+    const float* __restrict__ rois, float* __restrict__ acc_nhwc) {
+  const int ah = ph + 1, aw = pw + 1, P = ph * pw;
+  const int r = blockIdx.y, c0 = blockIdx.x * kNhwcThreads;
+  const int nc = min(kNhwcThreads, C - c0);
+  __shared__ int gy[8], gx[8];
+  __shared__ float ghr[8], gwr[8];
+  __shared__ bool gvy[8], gvx[8];
+  __shared__ float g7[kNhwcThreads * 49];
+  const float* ro = rois + r * 5;
+  const int t = threadIdx.x;
+  if (t < ah) align_axis(ro[2] * scale, ro[4] * scale, ah, t, H, &gy[t], &ghr[t], &gvy[t]);
+  if (t >= 32 && t < 32 + aw) {
+    const int p = t - 32;
+    align_axis(ro[1] * scale, ro[3] * scale, aw, p, W, &gx[p], &gwr[p], &gvx[p]);
+  }
+  const float* tp = top + ((size_t)r * C + c0) * P;
+  for (int e = t; e < nc * P; e += kNhwcThreads) g7[e] = tp[e] / 4.f;  // coalesced slab
+  __syncthreads();
+  if (t >= nc) return;
+  const int b = (int)ro[0];
+  float* base = acc_nhwc + (size_t)b * H * W * C + c0 + t;
+  const float* gp = g7 + t * P;
+  for (int sy = 0; sy < ah; ++sy) {
+    if (!gvy[sy]) continue;
+    const int y = gy[sy];
+    const float hr = ghr[sy];
+    for (int sx = 0; sx < aw; ++sx) {
+      if (!gvx[sx]) continue;
+      float g = 0.f;  // avg_pool2d backward: py outer, px inner
+      for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
+        for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
+      const int x = gx[sx];
+      const float wr = gwr[sx], om = 1.f - wr;
+      float* p00 = base + ((size_t)y * W + x) * C;
+      atomicAdd(p00, (float)(((double)g * (1. - (double)hr)) * (double)om));
+      atomicAdd(p00 + C, (float)(((double)g * (1. - (double)hr)) * (double)wr));
+      atomicAdd(p00 + (size_t)W * C, (g * hr) * om);
+      atomicAdd(p00 + (size_t)W * C + C, (g * hr) * wr);
+    }
+  }
+}
+
+// bottom_grad (B,C,H,W) += acc (B,H,W,C): 64x64 tiles through LDS.
+__global__ void __launch_bounds__(256) nhwc_add_to_nchw_kernel(const float* __restrict__ acc,
+                                                               int C, int HW,
+                                                               float* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z, p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const float* a = acc + (size_t)b * HW * C;
+  float* o = out + (size_t)b * C * HW;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int p = p0 + i, c = c0 + tx;
+    tile[i][tx] = (p < HW && c < C) ? a[(size_t)p * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, p = p0 + tx;
+    if (p < HW && c < C) o[(size_t)c * HW + p] += tile[tx][i];
+  }
+}
+
 // ------------------------------------------------------------ RoIPool
 __global__ void roi_pool_fwd_kernel(int total, const float* __restrict__ feat, float scale,
                                     int C, int H, int W, int PH, int PW,
@@ -272,14 +343,35 @@ extern "C" int tlod_roi_align_avg_fwd_f32(const float* feat, int B, int C, int H
   return kOk;
 }
 
+extern "C" size_t tlod_roi_align_avg_bwd_workspace_bytes(int B, int C, int H, int W) {
+  return (size_t)B * C * H * W * sizeof(float);
+}
+
 extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W,
                                           const float* rois, int R, int ph, int pw, float scale,
-                                          float* bottom_grad, tlod_stream_t stream) {
+                                          float* bottom_grad, void* ws, size_t ws_bytes,
+                                          tlod_stream_t stream) {
   TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0, "bad shape");
   TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
   if (R == 0) return kOk;
-  hipLaunchKernelGGL(roi_align_avg_bwd_kernel, dim3(div_up(C, kAvgCh), R), dim3(kAvgThreads), 0,
-                     (hipStream_t)stream, top_grad, scale, C, H, W, ph, pw, rois, bottom_grad);
+  hipStream_t s = (hipStream_t)stream;
+  if (ws == nullptr) {  // no workspace: accumulate straight into NCHW (slow atomic shape)
+    hipLaunchKernelGGL(roi_align_avg_bwd_kernel, dim3(div_up(C, kAvgCh), R), dim3(kAvgThreads), 0,
+                       s, top_grad, scale, C, H, W, ph, pw, rois, bottom_grad);
+    TLOD_LAUNCH_CHECK();
+    return kOk;
+  }
+  if (ws_bytes < (size_t)B * C * H * W * sizeof(float)) {
+    set_error("tlod_roi_align_avg_bwd_f32: workspace too small");
+    return kWorkspace;
+  }
+  float* acc = static_cast<float*>(ws);
+  TLOD_HIP(hipMemsetAsync(acc, 0, (size_t)B * C * H * W * sizeof(float), s));
+  hipLaunchKernelGGL(roi_align_avg_bwd_nhwc_kernel, dim3(div_up(C, kNhwcThreads), R),
+                     dim3(kNhwcThreads), 0, s, top_grad, scale, C, H, W, ph, pw, rois, acc);
+  TLOD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
+                     0, s, acc, C, H * W, bottom_grad);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

@@ -44,8 +44,9 @@ SIGNATURES = {
                                        c_float, P, P]),
     "tlod_roi_align_avg_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
                                            c_float, P, P]),
+    "tlod_roi_align_avg_bwd_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "tlod_roi_align_avg_bwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
-                                           c_float, P, P]),
+                                           c_float, P, P, c_size_t, P]),
     "tlod_roi_pool_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
                                       c_float, P, P, P]),
     "tlod_roi_pool_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "tlod_conv_wgrad_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                     c_size_t, P]),
     "tlod_relu_bwd_bias_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, P]),
+    "tlod_sgd_clip_f32": (c_int, [P, c_int, c_float, c_float, P, P, P]),
 }
 
 _lib = None

@@ -26,8 +26,10 @@ def build_daf_vgg16(device, classes=CITYSCAPES_CLASSES, seed=0):
     return m.to(device).train()
 
 
-def make_optimizer(model, lr, momentum=None, weight_decay=None, double_bias=None, bias_decay=None):
-    """DAF_train.py:311-325 param groups (collapsed to two groups — same update)."""
+def make_optimizer(model, lr, momentum=None, weight_decay=None, double_bias=None, bias_decay=None,
+                   fused=True, clip=10.0):
+    """DAF_train.py:311-325 param groups (collapsed to two groups — same update).
+    fused=True: libtlod's fused clip_gradient(clip) + SGD (tlod.optim.FusedSGDClip)."""
     momentum = cfg.TRAIN.MOMENTUM if momentum is None else momentum
     wd = cfg.TRAIN.WEIGHT_DECAY if weight_decay is None else weight_decay
     double_bias = cfg.TRAIN.DOUBLE_BIAS if double_bias is None else double_bias
@@ -39,6 +41,9 @@ def make_optimizer(model, lr, momentum=None, weight_decay=None, double_bias=None
     groups = [{"params": weights, "lr": lr, "weight_decay": wd},
               {"params": biases, "lr": lr * (double_bias + 1),
                "weight_decay": wd if bias_decay else 0.0}]
+    if fused:
+        from ..optim import FusedSGDClip
+        return FusedSGDClip(groups, momentum=momentum, clip_norm=clip)
     return torch.optim.SGD(groups, lr=lr, momentum=momentum, foreach=True)
 
 
@@ -117,9 +122,13 @@ def train_step(model, optimizer, batch, lamda=0.1, clip=10.0, reducer=None):
     loss.backward()
     if reducer is not None:
         reducer.finish()
-    if clip:
-        clip_gradient_([p for p in model.parameters()], clip)
-    optimizer.step()
+    from ..optim import FusedSGDClip
+    if isinstance(optimizer, FusedSGDClip):
+        optimizer.step()  # clip_gradient + SGD fused
+    else:
+        if clip:
+            clip_gradient_([p for p in model.parameters()], clip)
+        optimizer.step()
     return loss.detach()
 
 

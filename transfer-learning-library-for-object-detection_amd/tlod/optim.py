@@ -1,0 +1,79 @@
+"""Fused clip_gradient + SGD(momentum) on libtlod (tlod_sgd_clip_f32).
+
+Same update as ``clip_gradient(model, 10.)`` (lib/model/utils/net_utils.py:38-49) followed
+by ``torch.optim.SGD(params, momentum=0.9)`` with the reference's param groups
+(methods/DAF/DAF_train.py:311-325: biases lr*(DOUBLE_BIAS+1) and no weight decay unless
+BIAS_DECAY; weights lr and WEIGHT_DECAY) — three launches, no host synchronisation.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+CHUNK = 65536
+_DESC = np.dtype([("param", np.uint64), ("grad", np.uint64), ("buf", np.uint64),
+                  ("count", np.int64), ("lr", np.float32), ("wd", np.float32)])
+
+
+class FusedSGDClip:
+    """param_groups: list of dicts {params, lr, weight_decay} (torch.optim.SGD layout)."""
+
+    def __init__(self, param_groups, momentum=0.9, clip_norm=10.0):
+        self.param_groups = [dict(g, params=[p for p in g["params"] if p.requires_grad])
+                             for g in param_groups]
+        self.momentum = float(momentum)
+        self.clip_norm = float(clip_norm)
+        self.params = [p for g in self.param_groups for p in g["params"]]
+        for p in self.params:
+            _lib.require_cuda(p)
+        dev = self.params[0].device
+        self.bufs = [torch.zeros_like(p) for p in self.params]
+        n_chunks = sum((p.numel() + CHUNK - 1) // CHUNK for p in self.params)
+        self.partials = torch.empty(n_chunks, dtype=torch.float32, device=dev)
+        self.norm_scale = torch.zeros(2, dtype=torch.float32, device=dev)
+        self._key = None
+        self._table = None
+        self._host = torch.empty(n_chunks * _DESC.itemsize, dtype=torch.uint8).pin_memory()
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    def _chunk_table(self):
+        grads = [p.grad for p in self.params]
+        key = tuple(g.data_ptr() for g in grads) + tuple(g["lr"] for g in self.param_groups)
+        if key == self._key:
+            return self._table
+        rows = []
+        idx = 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                gr, buf = p.grad, self.bufs[idx]
+                assert gr.is_contiguous() and p.is_contiguous()
+                n = p.numel()
+                for off in range(0, n, CHUNK):
+                    rows.append((p.data_ptr() + 4 * off, gr.data_ptr() + 4 * off,
+                                 buf.data_ptr() + 4 * off, min(CHUNK, n - off), g["lr"],
+                                 g.get("weight_decay", 0.0)))
+                idx += 1
+        arr = np.array(rows, dtype=_DESC)
+        host = self._host[:arr.nbytes]
+        host.numpy()[:] = arr.view(np.uint8)
+        table = torch.empty(arr.nbytes, dtype=torch.uint8, device=self.partials.device)
+        table.copy_(host)  # rare (only when grad buffers move): a blocking copy is fine
+        self._key, self._table, self._n = key, table, len(rows)
+        return table
+
+    @torch.no_grad()
+    def step(self):
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        table = self._chunk_table()
+        _lib.check(_lib.lib().tlod_sgd_clip_f32(
+            _lib.ptr(table), self._n, self.momentum, self.clip_norm, _lib.ptr(self.partials),
+            _lib.ptr(self.norm_scale), _lib.stream_of(self.partials)), "sgd_clip")
+        return self.norm_scale[0]

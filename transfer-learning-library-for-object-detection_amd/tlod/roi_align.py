@@ -69,9 +69,12 @@ class RoIAlignAvgFunction(torch.autograd.Function):
         B, C, H, W, ph, pw, sc = ctx.meta
         g = grad_output.contiguous()
         grad_in = torch.zeros((B, C, H, W), dtype=g.dtype, device=g.device)
-        _lib.check(_lib.lib().tlod_roi_align_avg_bwd_f32(
+        L = _lib.lib()
+        ws = _lib.workspace(L.tlod_roi_align_avg_bwd_workspace_bytes(B, C, H, W), g.device,
+                            "roi_align_bwd")
+        _lib.check(L.tlod_roi_align_avg_bwd_f32(
             _lib.ptr(g), B, C, H, W, _lib.ptr(rois_c), rois_c.shape[0], ph, pw, sc,
-            _lib.ptr(grad_in), _lib.stream_of(g)), "roi_align_avg_bwd")
+            _lib.ptr(grad_in), _lib.ptr(ws), ws.numel(), _lib.stream_of(g)), "roi_align_avg_bwd")
         return grad_in, None, None, None, None
 
 
