@@ -96,51 +96,88 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
   const int a_base = khalf * C::HALF * C::BM + wm * MI * 32 + l32;
   const int b_base = khalf * (CK / 2) * C::PH * C::PW + wn * NJ * C::PW + l32;
 
-  float4 ra[C::A_PER];
-  float rb[C::B_PER];
+  // ---- staging (strength-reduced): every thread keeps fixed 32-bit offsets; per chunk
+  // only uniform bases change.  Loads are unconditional (invalid lanes read offset 0 of
+  // the same buffer) and the validity bits zero the values at LDS-store time, after the
+  // MFMA phase — a branch per load (or a select right after it) makes hipcc wait
+  // vmcnt(0) at the load instead of at the store.
+  constexpr int A_COLS = C::BM / 4;                 // float4 per A row
+  constexpr int A_ROWS_IT = C::NT / A_COLS;          // A rows per iteration
+  constexpr int A_IT = (C::KC + A_ROWS_IT - 1) / A_ROWS_IT;
+  constexpr int PP = C::PH * C::PW;                  // patch positions per channel
+  constexpr int B_PJ = (PP + C::NT - 1) / C::NT;     // positions per thread
+  const int a_kk = tid / A_COLS, a_mm = (tid % A_COLS) * 4;
+  const bool a_mok = m0 + a_mm < Cout;
+  const int a_off = a_kk * Cout + m0 + a_mm;
+  int b_r[B_PJ], b_c[B_PJ];
+#pragma unroll
+  for (int j = 0; j < B_PJ; ++j) {
+    const int pos = tid + j * C::NT;
+    b_r[j] = pos < PP ? pos / C::PW : 1 << 20;  // never in range when pos is past the patch
+    b_c[j] = pos % C::PW;
+  }
+  const int HWi = H * W;
+  float4 ra[A_IT];
+  float rb[B_PJ][CK];
+  unsigned amask = 0, bmask = 0;
 
-  // All staging loads are unconditional (out-of-range lanes read a clamped, valid
-  // address and select 0): a branch per load makes hipcc wait vmcnt(0) after each one.
   auto load_chunk = [&](int ch) {
     const int k0 = ch * C::KC;
+    const float* Ab = Wk + (size_t)k0 * Cout;
+    amask = 0;
 #pragma unroll
-    for (int i = 0; i < C::A_PER; ++i) {
-      const int e = tid + i * C::NT;
-      const int kk = e / (C::BM / 4), mm = (e % (C::BM / 4)) * 4;
-      const int k = k0 + kk, m = m0 + mm;
-      const bool ok = (e < C::A_V4) && (k < Ktot) && (m < Cout);
-      const float* src = ok ? Wk + (size_t)k * Cout + m : g_zero;
-      float4 v;
+    for (int i = 0; i < A_IT; ++i) {
+      const int kk = a_kk + i * A_ROWS_IT;
+      const bool ok = kk < C::KC && k0 + kk < Ktot && a_mok;
+      amask |= (unsigned)ok << i;
+      const int off = ok ? a_off + i * A_ROWS_IT * Cout : 0;
       if constexpr (VEC4) {
-        v = *reinterpret_cast<const float4*>(src);
-      } else {  // rows not 16-B aligned (e.g. dgrad of a 3-channel input)
-        v.x = src[0];
-        v.y = *((ok && m + 1 < Cout) ? src + 1 : g_zero);
-        v.z = *((ok && m + 2 < Cout) ? src + 2 : g_zero);
-        v.w = *((ok && m + 3 < Cout) ? src + 3 : g_zero);
+        ra[i] = *reinterpret_cast<const float4*>(Ab + off);
+      } else {  // rows not 16-B aligned (e.g. dgrad of a 3-channel input): rare path
+        const int m = m0 + a_mm;
+        ra[i].x = Ab[off];
+        ra[i].y = Ab[(ok && m + 1 < Cout) ? off + 1 : 0];
+        ra[i].z = Ab[(ok && m + 2 < Cout) ? off + 2 : 0];
+        ra[i].w = Ab[(ok && m + 3 < Cout) ? off + 3 : 0];
+        if (!(m + 1 < Cout)) ra[i].y = 0.f;  // masked below only per float4
+        if (!(m + 2 < Cout)) ra[i].z = 0.f;
+        if (!(m + 3 < Cout)) ra[i].w = 0.f;
       }
-      ra[i] = v;
     }
     const int ci0 = ch * CK;
+    const int base = (ci0 * H + h0 - pad) * W + (w0 - pad);
+    bmask = 0;
 #pragma unroll
-    for (int i = 0; i < C::B_PER; ++i) {
-      const int e = tid + i * C::NT;
-      const int ci = e / (C::PH * C::PW), r = (e / C::PW) % C::PH, c = e % C::PW;
-      const int gh = h0 - pad + r, gw = w0 - pad + c, gc = ci0 + ci;
-      const bool ok = (e < C::B_ELEMS) && gc < Cin && gh >= 0 && gh < H && gw >= 0 && gw < W;
-      rb[i] = *(ok ? Xn + ((size_t)gc * H + gh) * W + gw : g_zero);
+    for (int j = 0; j < B_PJ; ++j) {
+      const int gh = h0 - pad + b_r[j], gw = w0 - pad + b_c[j];
+      const bool pok = gh >= 0 && gh < H && gw >= 0 && gw < W;
+      const int poff = base + b_r[j] * W + b_c[j];
+#pragma unroll
+      for (int i = 0; i < CK; ++i) {
+        const bool ok = pok && ci0 + i < Cin;
+        bmask |= (unsigned)ok << (j * CK + i);
+        rb[j][i] = Xn[ok ? poff + i * HWi : 0];
+      }
     }
   };
   auto store_chunk = [&](float* As, float* Bs) {
 #pragma unroll
-    for (int i = 0; i < C::A_PER; ++i) {
-      const int e = tid + i * C::NT;
-      if (e < C::A_V4) reinterpret_cast<float4*>(As)[e] = ra[i];
+    for (int i = 0; i < A_IT; ++i) {
+      const int kk = a_kk + i * A_ROWS_IT;
+      if (kk < C::KC) {
+        const bool ok = (amask >> i) & 1;
+        reinterpret_cast<float4*>(As)[kk * A_COLS + a_mm / 4] =
+            ok ? ra[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < C::B_PER; ++i) {
-      const int e = tid + i * C::NT;
-      if (e < C::B_ELEMS) Bs[e] = rb[i];
+    for (int j = 0; j < B_PJ; ++j) {
+      const int pos = tid + j * C::NT;
+      if (pos < PP) {
+#pragma unroll
+        for (int i = 0; i < CK; ++i)
+          Bs[i * PP + pos] = ((bmask >> (j * CK + i)) & 1) ? rb[j][i] : 0.f;
+      }
     }
   };
 
@@ -283,46 +320,61 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
   }
   const int a_base = khalf * C::TW * C::GP + wm * MI * 32 + l32;
 
-  float rg[C::G_PER];
-  float rx[C::X_PER];
+  // ---- staging (strength-reduced, see conv_fwd_kernel)
+  constexpr int G_ROWS_IT = C::NT / C::P;            // G rows (channels) per iteration
+  constexpr int G_IT = C::BM / G_ROWS_IT;
+  constexpr int PP = C::PH * C::PW;
+  constexpr int X_CS = C::NT / PP > 0 ? C::NT / PP : 1;  // channel sub-groups
+  constexpr int X_IT = (C::NCI + X_CS - 1) / X_CS;
+  static_assert(C::NT % C::P == 0 && C::BM % G_ROWS_IT == 0, "G staging shape");
+  static_assert(PP <= C::NT, "X patch row must fit the workgroup");
+  const int g_p = tid % C::P, g_m = tid / C::P;
+  const int g_dh = g_p / C::TW, g_dw = g_p % C::TW;
+  const int x_pos = tid % PP, x_cs = tid / PP;
+  const bool x_act = x_cs < X_CS;
+  const int x_r = x_pos / C::PW, x_c = x_pos % C::PW;
+  const int HWi = H * W;
+  float rg[G_IT];
+  float rx[X_IT];
+  unsigned gmask = 0, xmask = 0;
+
   auto load_chunk = [&](int c) {
     const int cwi = c % cw, r = c / cw;
     const int chi = r % chh, n = r / chh;
     const int h0 = chi * C::TH, w0 = cwi * C::TW;
-    const float* Gn = G + (size_t)n * Cout * H * W;
-    const float* Xn = X + (size_t)n * Cin * H * W;
-    // unconditional loads from clamped addresses (see conv_fwd_kernel)
+    const float* Gn = G + (size_t)n * Cout * HWi;
+    const float* Xn = X + (size_t)n * Cin * HWi;
+    const bool pok = (h0 + g_dh < H) && (w0 + g_dw < W);
+    const int goff = (m0 + g_m) * HWi + (h0 + g_dh) * W + w0 + g_dw;
+    gmask = 0;
 #pragma unroll
-    for (int i = 0; i < C::G_PER; ++i) {
-      const int e = tid + i * C::NT;  // e -> (m, p), p fastest: 128-B row segments
-      const int m = e / C::P, p = e % C::P;
-      const int h = h0 + p / C::TW, w = w0 + p % C::TW;
-      const bool ok = (e < C::BM * C::P) && (m0 + m < Cout) && h < H && w < W;
-      rg[i] = *(ok ? Gn + ((size_t)(m0 + m) * H + h) * W + w : g_zero);
+    for (int i = 0; i < G_IT; ++i) {
+      const bool ok = pok && (m0 + g_m + i * G_ROWS_IT < Cout);
+      gmask |= (unsigned)ok << i;
+      rg[i] = Gn[ok ? goff + i * G_ROWS_IT * HWi : 0];
     }
+    const int gh = h0 - pad + x_r, gw = w0 - pad + x_c;
+    const bool xpok = x_act && gh >= 0 && gh < H && gw >= 0 && gw < W;
+    const int xoff = (cb + x_cs) * HWi + gh * W + gw;
+    xmask = 0;
 #pragma unroll
-    for (int i = 0; i < C::X_PER; ++i) {
-      const int e = tid + i * C::NT;
-      const int ci = e / (C::PH * C::PW), rr = (e / C::PW) % C::PH, cc = e % C::PW;
-      const int gc = cb + ci, gh = h0 - pad + rr, gw = w0 - pad + cc;
-      const bool ok = (e < C::NCI * C::PH * C::PW) && gc < Cin && gh >= 0 && gh < H && gw >= 0 &&
-                      gw < W;
-      rx[i] = *(ok ? Xn + ((size_t)gc * H + gh) * W + gw : g_zero);
+    for (int i = 0; i < X_IT; ++i) {
+      const int ci = x_cs + i * X_CS;
+      const bool ok = xpok && ci < C::NCI && cb + ci < Cin;
+      xmask |= (unsigned)ok << i;
+      rx[i] = Xn[ok ? xoff + i * X_CS * HWi : 0];
     }
   };
   auto store_chunk = [&](float* Gs, float* Xs) {
 #pragma unroll
-    for (int i = 0; i < C::G_PER; ++i) {
-      const int e = tid + i * C::NT;
-      if (e < C::BM * C::P) {
-        const int m = e / C::P, p = e % C::P;
-        Gs[p * C::GP + m] = rg[i];
-      }
-    }
+    for (int i = 0; i < G_IT; ++i)
+      Gs[g_p * C::GP + g_m + i * G_ROWS_IT] = ((gmask >> i) & 1) ? rg[i] : 0.f;
+    if (x_act) {
 #pragma unroll
-    for (int i = 0; i < C::X_PER; ++i) {
-      const int e = tid + i * C::NT;
-      if (e < C::NCI * C::PH * C::PW) Xs[e] = rx[i];
+      for (int i = 0; i < X_IT; ++i) {
+        const int ci = x_cs + i * X_CS;
+        if (ci < C::NCI) Xs[ci * PP + x_pos] = ((xmask >> i) & 1) ? rx[i] : 0.f;
+      }
     }
   };
 
