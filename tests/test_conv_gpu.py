@@ -72,9 +72,10 @@ def test_wgrad_deterministic():
 
 
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 512, 512, 37, 75), (1, 512, 512, 12, 20),
-                                            (2, 256, 512, 38, 40)])
+                                            (2, 256, 512, 38, 40), (1, 64, 256, 150, 250)])
 def test_conv_split_k_paths(N, Cin, Cout, H, W):
-    """Small spatial maps take the split-K path (slab + deterministic reduce)."""
+    """Small maps split every tile over input channels; larger ones (the last shape: 608
+    tiles on 512 slots) split only the tail round.  Both go through the slab + reduce."""
     from tlod import _lib
     from tlod.conv import conv_dgrad, conv_fwd
     assert _lib.lib().tlod_conv_fwd_workspace_bytes(N, Cin, H, W, Cout, 3) > 0

@@ -70,17 +70,30 @@ template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
 __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ Wk, const float* __restrict__ bias,
     float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int relu, int tiles_m,
-    int tiles_w, int tiles_h, int ksplit, int cps, float* __restrict__ slab) {
+    int tiles_w, int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 
-  const int nwg = tiles_m * tiles_w * tiles_h * N * ksplit;
-  int t = xcd_remap(blockIdx.x, nwg);
+  // Schedule: workgroups [0, dp_tiles) each own a whole output tile (full K); the
+  // remaining n_tail tiles are split ksplit ways over input-channel chunks, their raw
+  // partial sums going to slab[(split, tail tile)] (reduced by fwd_tail_reduce_kernel).
+  // Both ranges are XCD-remapped separately.
+  const int n_tiles = tiles_m * tiles_w * tiles_h * N;
+  const int n_tail = n_tiles - dp_tiles;
+  const bool direct = (int)blockIdx.x < dp_tiles;
+  int t, split = 0, ti = 0;
+  if (direct) {
+    t = xcd_remap(blockIdx.x, dp_tiles);
+  } else {
+    const int u = xcd_remap(blockIdx.x - dp_tiles, n_tail * ksplit);
+    ti = u % n_tail;
+    split = u / n_tail;
+    t = dp_tiles + ti;
+  }
   const int mt = t % tiles_m; t /= tiles_m;
   const int tw = t % tiles_w; t /= tiles_w;
   const int th = t % tiles_h; t /= tiles_h;
-  const int n = t % N;
-  const int split = t / N;  // split-K slice over input-channel chunks
+  const int n = t;
   const int m0 = mt * C::BM, w0 = tw * C::TW, h0 = th * C::TH;
   const int pad = KS / 2;
 
@@ -195,7 +208,8 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     const float bv = bias ? bias[co < Cout ? co : 0] : 0.f;
     bias_s[tid] = (bias && co < Cout) ? bv : 0.f;
   }
-  const int c_begin = split * cps, c_end = min(nchunks, c_begin + cps);
+  const int c_begin = direct ? 0 : split * cps;
+  const int c_end = direct ? nchunks : min(nchunks, c_begin + cps);
   if (c_begin < c_end) {
     load_chunk(c_begin);
     store_chunk(lds, lds + C::A_ELEMS);
@@ -232,10 +246,21 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
   }
 
   // epilogue: lane owns pixel column l32; rows (co) = (r&3) + 8*(r>>2) + 4*khalf.
-  // Split-K: raw partial sums go to slab[split] (bias/ReLU applied by the reduce).
-  float* Yn = (ksplit > 1 ? slab + (size_t)split * N * Cout * H * W : Y) + (size_t)n * Cout * H * W;
-  if (ksplit > 1) relu = 0;
-  const bool add_bias = bias && ksplit == 1;
+  constexpr int TP = C::TH * C::TW;  // pixels per tile
+  if (!direct) {  // raw partial sums, whole tile (the reduce bounds-checks)
+    float* St = slab + ((size_t)split * n_tail + ti) * C::BM * TP;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+          St[ml * TP + (wn * NJ + j) * C::TW + l32] = acc[i][j][r];
+        }
+    return;
+  }
+  float* Yn = Y + (size_t)n * Cout * H * W;
   const int w = w0 + l32;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -248,8 +273,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
         const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         const int co = m0 + ml;
         if (co < Cout) {
-          float v = acc[i][j][r];
-          if (add_bias) v += bias_s[ml];
+          float v = acc[i][j][r] + bias_s[ml];
           if (relu) v = fmaxf(v, 0.f);
           Yn[((size_t)co * H + h) * W + w] = v;
         }
@@ -261,28 +285,37 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
 // Block tile: BM = WM*MI*32 output channels x BN = WN*NJ*32 GEMM columns n=(ci,kh,kw);
 // K = pixels, chunked as TH=2 rows x 32 columns.  The MFMA pairs pixel (0, c) with
 // (1, c) (lanes 0-31 / 32-63): +1 row, a lane-constant offset.  grid.y = split-K slices.
-template <int WM, int WN, int MI, int NJ, int KS>
+template <int WM, int WN, int MI, int NJ, int KS, int TH_>
 struct WgCfg {
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * MI * 32;
   static constexpr int BN = WN * NJ * 32;
   static constexpr int KK = KS * KS;
-  static constexpr int TH = 2, TW = 32, P = TH * TW;  // 64 pixels per chunk
+  static constexpr int TH = TH_, TW = 32, P = TH * TW;  // pixels per chunk
+  static constexpr int KSTEPS = P / 2;
   static constexpr int PH = TH + KS - 1, PW = TW + KS - 1;
+  // LDS patch pitch: row pitch PWP = KS (mod 32) and channel stride CSTR = KK (mod 32), so
+  // the 32 consecutive GEMM columns (ci, kh, kw) a half-wave reads hit 32 distinct banks.
+  // (KS == 1: one tap per channel, so an odd channel stride suffices.)
+  static constexpr int PWP = KS == 1 ? PW : PW + (((KS - PW) % 32) + 32) % 32;
+  static constexpr int CSTR =
+      KS == 1 ? (PH * PW) | 1 : PH * PWP + (((KK - PH * PWP) % 32) + 32) % 32;
+  // MFMA k pairing: lanes 32-63 take pixel p + P/2 (next row if TH == 2, +16 cols if 1)
+  static constexpr int PAIR_X = (TH == 2) ? PWP : 16;
   static constexpr int NCI = BN / KK + 2;           // channels a column tile can span
   static constexpr int GP = BM + 1;                  // padded pitch of Gs[p][m]
   static constexpr int G_ELEMS = P * GP;
-  static constexpr int X_ELEMS = NCI * PH * PW + PW + 8;  // + a zero row for dead columns
-  static constexpr int G_PER = (BM * P + NT - 1) / NT;
-  static constexpr int X_PER = (NCI * PH * PW + NT - 1) / NT;
+  static constexpr int X_ELEMS = NCI * CSTR + 48;    // + a zero row for dead columns
   static constexpr int LDS_FLOATS = 2 * (G_ELEMS + X_ELEMS);
+  static_assert(TH == 1 || TH == 2, "TH");
+  static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
 };
 
-template <int WM, int WN, int MI, int NJ, int KS>
+template <int WM, int WN, int MI, int NJ, int KS, int TH>
 __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
     const float* __restrict__ G, const float* __restrict__ X, float* __restrict__ slab, int N,
     int Cin, int H, int W, int Cout, int tiles_m, int tiles_n, int splits, int chunks_per_split) {
-  using C = WgCfg<WM, WN, MI, NJ, KS>;
+  using C = WgCfg<WM, WN, MI, NJ, KS, TH>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 
   const int nwg = tiles_m * tiles_n * splits;
@@ -306,19 +339,19 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
 
   // per-lane B column offsets into Xs (+1 patch row for the khalf=1 pixel row); dead
   // columns read the zero row at the end of the patch
-  const int zero_row = C::NCI * C::PH * C::PW;
+  const int zero_row = C::NCI * C::CSTR;
   int boff[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = n0 + wn * NJ * 32 + j * 32 + l32;
     if (col < Ktot) {
       const int ci = col / C::KK - cb, s = col % C::KK;
-      boff[j] = (ci * C::PH + s / KS + khalf) * C::PW + s % KS;
+      boff[j] = ci * C::CSTR + (s / KS) * C::PWP + s % KS + khalf * C::PAIR_X;
     } else {
       boff[j] = zero_row;
     }
   }
-  const int a_base = khalf * C::TW * C::GP + wm * MI * 32 + l32;
+  const int a_base = khalf * (C::P / 2) * C::GP + wm * MI * 32 + l32;
 
   // ---- staging (strength-reduced, see conv_fwd_kernel)
   constexpr int G_ROWS_IT = C::NT / C::P;            // G rows (channels) per iteration
@@ -373,7 +406,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
 #pragma unroll
       for (int i = 0; i < X_IT; ++i) {
         const int ci = x_cs + i * X_CS;
-        if (ci < C::NCI) Xs[ci * PP + x_pos] = ((xmask >> i) & 1) ? rx[i] : 0.f;
+        if (ci < C::NCI) Xs[ci * C::CSTR + x_r * C::PWP + x_c] = ((xmask >> i) & 1) ? rx[i] : 0.f;
       }
     }
   };
@@ -404,7 +437,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
     const bool more = c + 1 < c_end;
     if (more) load_chunk(c + 1);
 #pragma unroll
-    for (int ks = 0; ks < C::TW; ++ks) {
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
       float a[MI], b[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) a[i] = Gl[ks * C::GP + i * 32];
@@ -454,16 +487,32 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
 }
 
 // y = act(sum_s slab[s] + bias), summed in split order (deterministic).
-__global__ void fwd_split_reduce_kernel(const float* __restrict__ slab, int ksplit, size_t count,
-                                        const float* __restrict__ bias, int Cout, int HW,
-                                        int relu, float* __restrict__ y) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
-       i += (size_t)gridDim.x * blockDim.x) {
-    float v = slab[i];
-    for (int k = 1; k < ksplit; ++k) v += slab[(size_t)k * count + i];
-    if (bias) v += bias[(i / HW) % Cout];
+// Sum the split-K partial tiles of the tail tiles in fixed split order (deterministic),
+// add bias, apply ReLU and scatter to Y.  One workgroup per (tail tile, 1024 elements).
+__global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
+    const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int th_rows,
+    int tiles_m, int tiles_w, int tiles_h, const float* __restrict__ bias, int Cout, int H, int W,
+    int relu, float* __restrict__ Y) {
+  const int tp = th_rows * 32, tile_elems = bm * tp;
+  const int per_tile = (tile_elems + 1023) / 1024;
+  const int ti = blockIdx.x / per_tile;
+  int t = dp_tiles + ti;
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int tw = t % tiles_w; t /= tiles_w;
+  const int th = t % tiles_h; t /= tiles_h;
+  const int n = t;
+  const size_t stride = (size_t)n_tail * tile_elems;
+  const float* S = slab + (size_t)ti * tile_elems;
+  for (int e = (blockIdx.x % per_tile) * 1024 + threadIdx.x;
+       e < min(tile_elems, (blockIdx.x % per_tile + 1) * 1024); e += 256) {
+    const int ml = e / tp, pix = e % tp;
+    const int co = mt * bm + ml, h = th * th_rows + pix / 32, w = tw * 32 + pix % 32;
+    if (co >= Cout || h >= H || w >= W) continue;
+    float v = S[e];
+    for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
+    if (bias) v += bias[co];
     if (relu) v = fmaxf(v, 0.f);
-    y[i] = v;
+    Y[(((size_t)n * Cout + co) * H + h) * W + w] = v;
   }
 }
 
@@ -535,24 +584,85 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
 }
 
 // ======================================================================= launchers
-struct FwdPlan { int tiles_m, tiles_w, tiles_h, ksplit, cps; };
+// Tile-variant knobs for A/B measurement (read once; defaults are the tuned choices).
+static int tune_knob(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+
+struct FwdPlan {
+  int tiles_m, tiles_w, tiles_h;
+  int dp_tiles;  // tiles computed whole (full K)
+  int ksplit;    // split count of the remaining tail tiles (1: no tail)
+  int cps;       // input-channel chunks per split piece
+  int n_tail() const { return tiles_m * tiles_w * tiles_h * n - dp_tiles; }
+  int n;
+  size_t slab_bytes(int bm, int th) const {
+    return ksplit > 1 ? (size_t)ksplit * n_tail() * bm * th * 32 * sizeof(float) : 0;
+  }
+};
+
+// Resident workgroup slots of a kernel on this device (occupancy x CUs); callers cache
+// the result per kernel.  Without a device (CPU build checks) assume 256 (1 block/CU).
+template <typename K>
+static int resident_slots(K kern, int threads, size_t lds) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess ||
+      per_cu < 1 || cus < 1) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  return per_cu * cus;
+}
+
+// Wave quantization: a grid of T whole tiles on S resident slots runs ceil(T/S) rounds,
+// so e.g. conv3_3 (1216 tiles on 512 slots) idles 21% of the chip in its last round.
+// The last partial round (or, for small maps, every tile) is instead split over input
+// channels into ksplit pieces that fill the slots, at the cost of a slab round trip
+// through HBM.  Cost model in seconds: tiles at ~65% of the f32 MFMA peak per slot,
+// slab traffic (k writes + k reads + 1 write per tail tile) at 4 TB/s, 6 us per reduce.
+static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int nchunks,
+                             double tile_flops, int tile_elems, int slots) {
+  FwdPlan p{tiles_m, tiles_w, tiles_h, 0, 1, nchunks, N};
+  const long long T = (long long)tiles_m * tiles_w * tiles_h * N;
+  p.dp_tiles = (int)T;
+  const double tile_s = tile_flops / (157.3e12 * 0.65 / slots);
+  double best = (double)((T + slots - 1) / slots) * tile_s;
+  const int kmax = std::min(8, nchunks / 2);
+  const long long q = T / slots;
+  for (int k = 2; k <= kmax; ++k) {
+    const int cps = div_up(nchunks, k);
+    const int kk = div_up(nchunks, cps);
+    for (long long dp : {q * slots, 0ll}) {
+      const long long tail = T - dp;
+      if (tail <= 0) continue;
+      const double piece_s = tile_s * cps / nchunks;
+      const double t = (double)dp / slots * tile_s +
+                       (double)((tail * kk + slots - 1) / slots) * piece_s +
+                       (2.0 * kk + 1.0) * tail * tile_elems * 4.0 / 4e12 + 6e-6;
+      if (t < best * 0.97) {
+        best = t;
+        p.dp_tiles = (int)dp;
+        p.ksplit = kk;
+        p.cps = cps;
+      }
+    }
+  }
+  return p;
+}
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS>
 static FwdPlan plan_fwd(int N, int Cin, int H, int W, int Cout) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
-  FwdPlan p;
-  p.tiles_m = div_up(Cout, C::BM);
-  p.tiles_w = div_up(W, C::TW);
-  p.tiles_h = div_up(H, C::TH);
+  static const int slots = resident_slots(conv_fwd_kernel<WM, WN, MI, NJ, CK, KS, true>, C::NT,
+                                          C::LDS_FLOATS * sizeof(float));
   const int nchunks = div_up(Cin, CK);
-  const long long base = (long long)p.tiles_m * p.tiles_w * p.tiles_h * N;
-  // split K over input-channel chunks when the output tiles alone cannot fill ~3 waves
-  // of workgroups on the 256 CUs (conv5 / RPN at 37x75: 120 tiles)
-  int ks = 1;
-  if (base < 512) ks = (int)std::min<long long>(std::min(8, std::max(1, nchunks / 4)), div_up(768, (int)base));
-  p.cps = div_up(nchunks, ks);
-  p.ksplit = div_up(nchunks, p.cps);
-  return p;
+  return plan_schedule(div_up(Cout, C::BM), div_up(W, C::TW), div_up(H, C::TH), N, nchunks,
+                       2.0 * C::BM * C::TH * C::TW * (double)nchunks * C::KC,
+                       C::BM * C::TH * C::TW, slots);
 }
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
@@ -561,10 +671,9 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
                       hipStream_t s) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
   const FwdPlan p = plan_fwd<WM, WN, MI, NJ, CK, KS>(N, Cin, H, W, Cout);
-  const long long nwg = (long long)p.tiles_m * p.tiles_w * p.tiles_h * N * p.ksplit;
+  const long long nwg = (long long)p.dp_tiles + (long long)p.n_tail() * (p.ksplit > 1 ? p.ksplit : 0);
   TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
-  const size_t out_elems = (size_t)N * Cout * H * W;
-  if (p.ksplit > 1 && slab_bytes < p.ksplit * out_elems * sizeof(float)) {
+  if (p.ksplit > 1 && slab_bytes < p.slab_bytes(C::BM, C::TH)) {
     set_error("tlod_conv: workspace too small for split-K");
     return kWorkspace;
   }
@@ -576,12 +685,14 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
     attr = true;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wk, bias, Y, N, Cin, H, W,
-                     Cout, relu, p.tiles_m, p.tiles_w, p.tiles_h, p.ksplit, p.cps, slab);
+                     Cout, relu, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps,
+                     slab);
   TLOD_LAUNCH_CHECK();
   if (p.ksplit > 1) {
-    const int blocks = (int)std::min<size_t>((out_elems + 255) / 256, 4096);
-    hipLaunchKernelGGL(fwd_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, p.ksplit,
-                       out_elems, bias, Cout, H * W, relu, Y);
+    const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
+    hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
+                       p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
+                       p.tiles_h, bias, Cout, H, W, relu, Y);
     TLOD_LAUNCH_CHECK();
   }
   return kOk;
@@ -604,8 +715,9 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias,
 #define TLOD_FWD_CFG(WM_, WN_, MI_, NJ_, CK_, KS_)                                              \
   do {                                                                                          \
     if (ws_query) {                                                                             \
-      const FwdPlan p = plan_fwd<WM_, WN_, MI_, NJ_, CK_, KS_>(N, Cin, H, W, Cout);             \
-      *ws_query = p.ksplit > 1 ? (size_t)p.ksplit * N * Cout * H * W * sizeof(float) : 0;       \
+      using C_ = FwdCfg<WM_, WN_, MI_, NJ_, CK_, KS_>;                                          \
+      *ws_query = plan_fwd<WM_, WN_, MI_, NJ_, CK_, KS_>(N, Cin, H, W, Cout)                    \
+                      .slab_bytes(C_::BM, C_::TH);                                              \
       return kOk;                                                                               \
     }                                                                                           \
     return launch_fwd_v<WM_, WN_, MI_, NJ_, CK_, KS_>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, \
@@ -613,6 +725,7 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias,
   } while (0)
   if (KS == 3) {
     if (Cout <= 64) TLOD_FWD_CFG(1, 8, 2, 2, 8, 3);
+    if (tune_knob("TLOD_CONV_FWD_CK", 8) == 4) TLOD_FWD_CFG(2, 4, 2, 2, 4, 3);
     TLOD_FWD_CFG(2, 4, 2, 2, 8, 3);
   }
   if (KS == 1) {
@@ -624,33 +737,66 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias,
   return kUnsupported;
 }
 
-template <int WM, int WN, int MI, int NJ, int KS>
-static int launch_wgrad(const float* G, const float* X, float* slab, int splits, int N, int Cin,
-                        int H, int W, int Cout, hipStream_t s) {
-  using C = WgCfg<WM, WN, MI, NJ, KS>;
-  const int Ktot = Cin * C::KK;
-  const int tiles_m = div_up(Cout, C::BM), tiles_n = div_up(Ktot, C::BN);
-  const int total_chunks = N * div_up(H, C::TH) * div_up(W, C::TW);
-  const int cps = div_up(total_chunks, splits);
-  const int nwg = tiles_m * tiles_n * splits;
-  const size_t lds = C::LDS_FLOATS * sizeof(float);
-  auto kern = conv_wgrad_kernel<WM, WN, MI, NJ, KS>;
-  static bool attr = false;
-  if (!attr) {
-    TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
+// Split count over pixel chunks: the weight-gradient tiles alone (Cout/128 x 9Cin/256 =
+// 18 for conv3_3) cannot fill the chip, so the reduction over pixels is split into slabs.
+// Pick the count whose grid best fills whole rounds of resident workgroups (a grid of
+// 1.04 rounds runs as long as 2), keeping >= 8 pixel chunks per workgroup.
+static int pick_splits(int tiles, int chunks, int slots) {
+  const int smax = std::max(1, std::min(64, chunks / 8));
+  int best = 1;
+  double best_eff = -1.0;
+  for (int sp = 1; sp <= smax; ++sp) {
+    const long long nwg = (long long)tiles * sp;
+    const long long rounds = (nwg + slots - 1) / slots;
+    const double eff = (double)nwg / (double)(rounds * slots);
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = sp; }
   }
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), lds, s, G, X, slab, N, Cin, H, W, Cout, tiles_m,
-                     tiles_n, splits, cps);
-  TLOD_LAUNCH_CHECK();
-  return kOk;
+  return best;
 }
 
-int wgrad_splits(int N, int Cin, int H, int W, int Cout, int KS) {
-  const int tiles = div_up(Cout, 128) * div_up(Cin * KS * KS, 256);
-  const int chunks = N * div_up(H, 2) * div_up(W, 32);
-  int splits = std::max(1, std::min(chunks / 8, div_up(512, tiles)));
-  return std::min(splits, 64);
+template <int WM, int WN, int MI, int NJ, int KS, int TH>
+struct Wgrad {
+  using C = WgCfg<WM, WN, MI, NJ, KS, TH>;
+  static constexpr size_t kLds = C::LDS_FLOATS * sizeof(float);
+  static int splits(int N, int Cin, int H, int W, int Cout) {
+    const int tiles = div_up(Cout, C::BM) * div_up(Cin * C::KK, C::BN);
+    const int chunks = N * div_up(H, C::TH) * div_up(W, C::TW);
+    static const int slots =
+        resident_slots(conv_wgrad_kernel<WM, WN, MI, NJ, KS, TH>, C::NT, kLds);
+    return pick_splits(tiles, chunks, slots);
+  }
+  static int launch(const float* G, const float* X, float* slab, int splits, int N, int Cin,
+                    int H, int W, int Cout, hipStream_t s) {
+    const int Ktot = Cin * C::KK;
+    const int tiles_m = div_up(Cout, C::BM), tiles_n = div_up(Ktot, C::BN);
+    const int total_chunks = N * div_up(H, C::TH) * div_up(W, C::TW);
+    const int cps = div_up(total_chunks, splits);
+    const int nwg = tiles_m * tiles_n * splits;
+    auto kern = conv_wgrad_kernel<WM, WN, MI, NJ, KS, TH>;
+    static bool attr = false;
+    if (!attr) {
+      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), kLds, s, G, X, slab, N, Cin, H, W, Cout,
+                       tiles_m, tiles_n, splits, cps);
+    TLOD_LAUNCH_CHECK();
+    return kOk;
+  }
+};
+
+// The wgrad tile config per kernel size (TLOD_CONV_WGRAD_TH=2 selects the 2-row variant).
+template <typename F>
+static int with_wgrad_cfg(int KS, F&& f) {
+  static const int th = tune_knob("TLOD_CONV_WGRAD_TH", 1) == 2 ? 2 : 1;
+  if (KS == 3 && th == 1) return f(Wgrad<2, 4, 2, 2, 3, 1>{});
+  if (KS == 3) return f(Wgrad<2, 4, 2, 2, 3, 2>{});
+  if (KS == 1) return f(Wgrad<2, 2, 2, 2, 1, 2>{});
+  return -1;
+}
+
+static int wgrad_splits(int N, int Cin, int H, int W, int Cout, int KS) {
+  return with_wgrad_cfg(KS, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
 }
 
 }  // namespace tlod
@@ -706,7 +852,8 @@ extern "C" int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, 
 }
 
 extern "C" size_t tlod_conv_wgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS) {
-  return (size_t)wgrad_splits(N, Cin, H, W, Cout, KS) * Cout * Cin * KS * KS * sizeof(float);
+  const int sp = wgrad_splits(N, Cin, H, W, Cout, KS);
+  return sp > 0 ? (size_t)sp * Cout * Cin * KS * KS * sizeof(float) : 0;
 }
 
 extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, int accumulate,
@@ -715,16 +862,16 @@ extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, i
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
   TLOD_CHECK_ARG((Cout * Cin * KS * KS) % 4 == 0, "Cout*Cin*KS*KS must be a multiple of 4");
   hipStream_t s = (hipStream_t)stream;
+  TLOD_CHECK_ARG(KS == 1 || KS == 3, "conv wgrad: only 1x1 and 3x3 kernels");
   const int splits = wgrad_splits(N, Cin, H, W, Cout, KS);
   if (ws_bytes < (size_t)splits * Cout * Cin * KS * KS * sizeof(float)) {
     set_error("tlod_conv_wgrad_f32: workspace too small");
     return kWorkspace;
   }
   float* slab = static_cast<float*>(ws);
-  int st;
-  if (KS == 3) st = launch_wgrad<2, 4, 2, 2, 3>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
-  else if (KS == 1) st = launch_wgrad<2, 2, 2, 2, 1>(dy, x, slab, splits, N, Cin, H, W, Cout, s);
-  else { set_error("conv wgrad: only 1x1 and 3x3"); return kUnsupported; }
+  const int st = with_wgrad_cfg(KS, [&](auto cfg) {
+    return cfg.launch(dy, x, slab, splits, N, Cin, H, W, Cout, s);
+  });
   if (st) return st;
   const size_t count = (size_t)Cout * Cin * KS * KS;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count / 4 + 255) / 256, 2048)),
