@@ -44,15 +44,21 @@ def parse():
 
 def conv_roofline(records):
     """Aggregate the timed conv launches: algorithmic FLOPs / measured kernel time."""
-    tot_f, tot_ms, by = 0.0, 0.0, {}
-    for s, e, flops, kind in records:
+    tot_f, tot_ms, by, shapes = 0.0, 0.0, {}, {}
+    for s, e, flops, kind, shape in records:
         ms = s.elapsed_time(e)
         tot_f += flops
         tot_ms += ms
-        d = by.setdefault(kind, [0.0, 0.0, 0])
-        d[0] += flops
-        d[1] += ms
-        d[2] += 1
+        for key, table in ((kind, by), ((kind,) + tuple(shape), shapes)):
+            d = table.setdefault(key, [0.0, 0.0, 0])
+            d[0] += flops
+            d[1] += ms
+            d[2] += 1
+    if os.environ.get("TLOD_BENCH_SHAPES"):
+        for k, v in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
+            print(f"{k[0]:6s} N={k[1]} Cin={k[2]:4d} {k[3]:4d}x{k[4]:<4d} Cout={k[5]:4d} KS={k[6]} "
+                  f"launches={v[2]:4d} ms={v[1]:8.3f} TF={v[0] / (v[1] * 1e-3) / 1e12:7.2f}",
+                  file=sys.stderr)
     if tot_ms == 0:
         return 0.0, {}, 0.0, 0.0, 0
     achieved = tot_f / (tot_ms * 1e-3) / 1e12

@@ -20,18 +20,20 @@ import torch.nn.functional as F
 from . import _lib
 
 
-# Optional launch timing (bench.py): list of (start_event, end_event, flops, kind) or None.
+# Optional launch timing (bench.py): list of (start_event, end_event, flops, kind, shape)
+# or None; shape = (N, Cin, H, W, Cout, KS).
 PROFILE = None
 
 
-def _timed(kind, flops, fn):
+def _timed(kind, shape, fn):
     if PROFILE is None:
         return fn()
+    N, Cin, H, W, Cout, KS = shape
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     r = fn()
     e.record()
-    PROFILE.append((s, e, flops, kind))
+    PROFILE.append((s, e, 2.0 * N * H * W * Cout * Cin * KS * KS, kind, shape))
     return r
 
 
@@ -69,7 +71,7 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None):
     b = bias.detach().contiguous() if bias is not None else None
     L = _lib.lib()
     ws = _lib.workspace(L.tlod_conv_fwd_workspace_bytes(N, Cin, H, W, Cout, KS), x.device, "conv")
-    _timed("fwd", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
+    _timed("fwd", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
         L.tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N, Cin, H, W, Cout,
                             KS, int(relu), _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv_fwd"))
     return y
@@ -83,7 +85,7 @@ def conv_dgrad(g, weight, wd=None):
     dx = torch.empty((N, Cin, H, W), dtype=torch.float32, device=g.device)
     L = _lib.lib()
     ws = _lib.workspace(L.tlod_conv_dgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "conv")
-    _timed("dgrad", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
+    _timed("dgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
         L.tlod_conv_dgrad_f32(_lib.ptr(g), _lib.ptr(wd), _lib.ptr(dx), N, Cin, H, W, Cout, KS,
                               _lib.ptr(ws), ws.numel(), _lib.stream_of(g)), "conv_dgrad"))
     return dx
@@ -98,7 +100,7 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False):
     dw = out if out is not None else torch.empty((Cout, Cin, KS, KS), dtype=torch.float32,
                                                  device=g.device)
     ws = _lib.workspace(L.tlod_conv_wgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "wgrad")
-    _timed("wgrad", 2.0 * N * H * W * Cout * Cin * KS * KS, lambda: _lib.check(
+    _timed("wgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
         L.tlod_conv_wgrad_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin, H, W,
                               Cout, KS, _lib.ptr(ws), ws.numel(), _lib.stream_of(g)), "conv_wgrad"))
     return dw
