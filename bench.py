@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-baseline-steps", type=int, default=2,
                     help="oracle CPU steps timed on rank 0 at N=1 (0 disables)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--method", choices=("daf", "maf"), default="daf",
+                    help="detector (the headline metric is DAF; MAF is a secondary workload)")
     return ap.parse_args()
 
 
@@ -84,14 +86,14 @@ def main():
     a = parse()
     from tlod.dist import GradBucketReducer, init_from_env
     from tlod import conv as tconv
-    from tlod.detector.train import (SyntheticCityscapes, build_daf_vgg16, make_optimizer,
+    from tlod.detector.train import (SyntheticCityscapes, build_model, make_optimizer,
                                      train_step)
 
     rank, world = init_from_env()
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    model = build_daf_vgg16(dev)
+    model = build_model(a.method, dev)
     opt = make_optimizer(model, 2e-3)
     reducer = GradBucketReducer(model, bucket_mb=a.bucket_mb) if world > 1 else None
     data = SyntheticCityscapes(dev, H=a.height, W=a.width, seed=1000 * rank + 1)
@@ -124,11 +126,13 @@ def main():
 
     achieved, detail, conv_ms, conv_f, n_launch = conv_roofline(records)
     result = {
-        "metric": METRIC, "value": round(value, 4), "unit": "img/s", "n_gpus": world,
+        "metric": METRIC if a.method == "daf" else METRIC.replace("DAF", a.method.upper()),
+        "value": round(value, 4), "unit": "img/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": "DAF VGG16 Cityscapes->Foggy training step (methods/DAF/DAF_train.py), "
+        "config": {"workload": f"{a.method.upper()} VGG16 Cityscapes->Foggy training step "
+                               f"(methods/{a.method.upper()}/{a.method.upper()}_train.py), "
                                "1 source + 1 target image per GPU per step",
                    "image_hw": [a.height, a.width], "source_images_per_step": world,
                    "images_processed_per_step": 2 * world, "parallelism": f"dp{world}",
@@ -143,7 +147,7 @@ def main():
         "mean_loss": round(last_loss, 4),
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and a.cpu_baseline_steps > 0:
+    if rank == 0 and world == 1 and a.cpu_baseline_steps > 0 and a.method == "daf":
         result["cpu_baseline"] = cpu_baseline(a.cpu_baseline_steps, a.height, a.width)
     if rank == 0:
         print(json.dumps(result), flush=True)

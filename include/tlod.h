@@ -243,6 +243,18 @@ typedef struct tlod_sgd_chunk {
 int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float momentum,
                       float clip_norm, float* partials, float* norm_scale, tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ MAF DRM
+ * Replaces: the chunk / reshape / cat loops of DRM.forward, lib/MAF/drm.py:23-40 (a
+ *   Python double loop over (H/s)*(W/s) chunks).  x: (B, C, H, W); the map is cropped
+ *   to Ho = floor(H/s), Wo = floor(W/s) blocks (drm.py:23-26) and
+ *   y[b, c*s*s + i*s + j, h, w] = x[b, c, h*s + i, w*s + j]   (y: B x C*s*s x Ho x Wo),
+ *   i.e. pixel_unshuffle of the cropped map.  depth_to_space is its adjoint: dx gets dy
+ *   scattered back and zeros on the cropped-away border. */
+int tlod_space_to_depth_f32(const float* x, int B, int C, int H, int W, int scale, float* y,
+                            tlod_stream_t stream);
+int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int W, int scale, float* dx,
+                            tlod_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -110,13 +110,21 @@ class OracleDAF(nn.Module):
         x = F.dropout(F.relu(m.dc_ip2(x)), self.dropout, self.training)
         return torch.sigmoid(m.clssifer(x))
 
-    def forward(self, batch, rng, rois_override=None):
-        """rois_override: (source proposals (1,2000,5), target proposals (1,300,5)) taken
-        from the device run, so float-order differences in the score sort cannot fork
-        the sampled RoIs between the two implementations."""
+    def _backbone(self, im):
+        """RCNN_base in the three pieces MAF taps (lib/MAF/vgg16.py:84-86): conv3 =
+        features[:16], conv34 = [16:23], conv45 = [23:-1]."""
+        c3 = self.RCNN_base[:16](im)
+        c4 = self.RCNN_base[16:23](c3)
+        return c3, c4, self.RCNN_base[23:](c4)
+
+    def _detect(self, batch, rng, rois_override=None):
+        """Everything but the DA heads (lib/DAF/faster_rcnn.py:45-175).  rois_override:
+        (source proposals (1,2000,5), target proposals (1,300,5)) taken from the device
+        run, so float-order differences in the score sort cannot fork the sampled RoIs
+        between the two implementations."""
         (im, info, gt, num, need, t_im, t_info, t_gt, t_num, t_need) = batch
         c = CFG
-        base = self.RCNN_base(im)
+        c3, c4, base = self._backbone(im)
         score, sr, prob, bbox = self._rpn(base)
         rois = orpn.proposal_layer(prob.detach().numpy(), bbox.detach().numpy(), info.numpy(),
                                    self.base_anchors, c["stride"], c["pre_train"], c["post_train"],
@@ -143,7 +151,7 @@ class OracleDAF(nn.Module):
         rcnn_box = _smooth_l1(bp, torch.from_numpy(rt).view(-1, 4), torch.from_numpy(riw).view(-1, 4),
                               torch.from_numpy(row).view(-1, 4))
         # target image: RPN in eval mode (TEST proposals)
-        t_base = self.RCNN_base(t_im)
+        t_c3, t_c4, t_base = self._backbone(t_im)
         _, _, t_prob, t_bbox = self._rpn(t_base)
         t_rois = orpn.proposal_layer(t_prob.detach().numpy(), t_bbox.detach().numpy(),
                                      t_info.numpy(), self.base_anchors, c["stride"], c["pre_test"],
@@ -152,6 +160,13 @@ class OracleDAF(nn.Module):
             t_rois = rois_override[1]
         t_pooled = _RoIAlignAvgCPU.apply(t_base, torch.from_numpy(t_rois).view(-1, 5))
         t_fc7 = self.RCNN_top(t_pooled.view(t_pooled.size(0), -1))
+        return dict(rpn_loss_cls=rpn_loss_cls, rpn_loss_box=rpn_loss_box, RCNN_loss_cls=rcnn_cls,
+                    RCNN_loss_bbox=rcnn_box, rois=r, c3=c3, c4=c4, base=base, fc7=fc7, cls=cls,
+                    t_c3=t_c3, t_c4=t_c4, t_base=t_base, t_fc7=t_fc7)
+
+    def forward(self, batch, rng, rois_override=None):
+        d = self._detect(batch, rng, rois_override)
+        base, fc7, t_base, t_fc7 = d["base"], d["fc7"], d["t_base"], d["t_fc7"]
         # DA (faster_rcnn.py:181-220)
         bs = self._image_da(base)
         da_img = F.nll_loss(F.log_softmax(bs, 1), torch.ones(bs.shape[0], *bs.shape[2:], dtype=torch.long))
@@ -167,10 +182,11 @@ class OracleDAF(nn.Module):
         t_da_ins = F.binary_cross_entropy(t_ins, y)
         t_cst = F.softmax(tbs, 1)[:, 0].mean().detach()
         t_da_cst = ((t_ins - t_cst) ** 2).sum()
-        return dict(rpn_loss_cls=rpn_loss_cls, rpn_loss_box=rpn_loss_box, RCNN_loss_cls=rcnn_cls,
-                    RCNN_loss_bbox=rcnn_box, DA_img_loss_cls=da_img, DA_ins_loss_cls=da_ins,
+        return dict(rpn_loss_cls=d["rpn_loss_cls"], rpn_loss_box=d["rpn_loss_box"],
+                    RCNN_loss_cls=d["RCNN_loss_cls"], RCNN_loss_bbox=d["RCNN_loss_bbox"],
+                    DA_img_loss_cls=da_img, DA_ins_loss_cls=da_ins,
                     tgt_DA_img_loss_cls=t_da_img, tgt_DA_ins_loss_cls=t_da_ins, DA_cst_loss=da_cst,
-                    tgt_DA_cst_loss=t_da_cst, rois=r)
+                    tgt_DA_cst_loss=t_da_cst, rois=d["rois"])
 
 
 def total_loss(o, lamda=0.1):

@@ -42,7 +42,7 @@ def test_host_only_calls():
     from tlod import _lib
     L = _lib.lib()
     assert L.tlod_abi_version() == 1
-    assert L.tlod_nms_workspace_bytes(12000) == 12000 * 188 * 8
+    assert L.tlod_nms_workspace_bytes(12000) >= 12000 * 188 * 8
     assert L.tlod_proposal_workspace_bytes(1, 12, 37, 75, 12000) > 0
     assert L.tlod_anchor_target_workspace_bytes(1, 12, 37, 75, 50) > 0
 

@@ -26,7 +26,8 @@ def _nms(d, thr, max_keep=0):
                                         (6000, 0.7, "clustered"), (300, 0.3, "clustered"),
                                         (65, 0.5, "clustered"), (64, 0.5, "clustered"),
                                         (1, 0.7, "random"), (2000, 0.0, "random"),
-                                        (3000, 1.0, "clustered")])
+                                        (3000, 1.0, "clustered"), (16384, 0.7, "clustered"),
+                                        (20000, 0.6, "clustered")])
 def test_nms_bit_exact(n, thr, kind):
     rng = np.random.default_rng(n + int(thr * 10))
     boxes = clustered_boxes(rng, n) if kind == "clustered" else random_boxes(rng, n)

@@ -85,3 +85,16 @@ def test_roi_pool_adjoint():
     g = rng.standard_normal(o.shape).astype(np.float32)
     gb = oroi.roi_pool_bwd(g, a, r, 1, 3, 9, 9, 1 / 16)
     np.testing.assert_allclose((o * g).sum(), (f * gb).sum(), rtol=1e-4)
+
+
+def test_drm_chunks_is_cropped_pixel_unshuffle():
+    """The literal DRM restatement (lib/MAF/drm.py:23-40) equals pixel_unshuffle of the
+    map cropped to whole s x s blocks: channel c*s*s + i*s + j <- (h*s + i, w*s + j)."""
+    import torch
+    import torch.nn.functional as F
+    from oracle.maf_step import drm_chunks
+    x = torch.randn(2, 5, 11, 14)
+    for s in (2, 3, 4):
+        Ho, Wo = 11 // s, 14 // s
+        ref = F.pixel_unshuffle(x[:, :, :Ho * s, :Wo * s], s)
+        assert torch.equal(drm_chunks(x, s), ref)

@@ -26,10 +26,12 @@ __device__ __forceinline__ float dev_iou(float a0, float a1, float a2, float a3,
 }
 
 // grid (col_blocks, row_blocks), block 64.  mask[i * col_blocks + cb] bit j set iff
-// box i suppresses box cb*64+j (j > i).
+// box i suppresses box cb*64+j (j > i).  Diagonal tiles also write the transposed
+// words: diag_t[b * 64 + j] bit i set iff box b*64+i suppresses box b*64+j (i < j).
 __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ boxes, int n,
                                                       int dim, float thresh,
                                                       unsigned long long* __restrict__ mask,
+                                                      unsigned long long* __restrict__ diag_t,
                                                       int col_blocks) {
   const int rb = blockIdx.y, cb = blockIdx.x;
   if (cb < rb) return;  // never read by the scan
@@ -54,12 +56,118 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
     }
     mask[(size_t)i * col_blocks + cb] = bits;
   }
+  if (rb == cb && t < col_size) {  // same IoU(a = row box, b = column box) as above
+    const float4 b = cols[t];
+    unsigned long long bits = 0;
+    for (int i = 0; i < t; ++i) {
+      const float4 a = cols[i];
+      if (dev_iou(a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w) > thresh) bits |= 1ull << i;
+    }
+    diag_t[cb * 64 + t] = bits;
+  }
 }
 
 constexpr int kScanThreads = 1024;
 constexpr int kMaxColBlocks = 2048;  // n <= 131072
+constexpr int kFastColBlocks = 256;  // n <= 16384: the pipelined scan below
 
-// One workgroup.  remv[] (removal bits per 64-box block) lives in LDS.  Block b's
+// Pipelined greedy scan for n <= 16384 (the proposal layer: 12000 / 6000 boxes).
+// Thread (g = t/256, c = t%256) owns mask column c for rows g*16..g*16+15 of each 64-row
+// block.  Those 16 words do not depend on the scan's outcome, so they are prefetched two
+// blocks ahead into registers.  Within a block, wave 0 solves the greedy recurrence
+//   kept_j = cand_j AND NOT OR_{i<j} (kept_i AND sup(i, j))
+// as a fixed-point iteration over the 64 lanes (lane j holds its suppressor column
+// diag_t): the recurrence has a unique solution, iterate k fixes lanes < k, so it
+// converges in <= 64 ballots and usually in 2-3 (identical to the sequential scan).
+__global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
+    const unsigned long long* __restrict__ mask, const unsigned long long* __restrict__ diag_t,
+    int n, int col_blocks, int max_keep, int32_t* __restrict__ keep,
+    int32_t* __restrict__ num_keep) {
+  __shared__ unsigned long long remv[kFastColBlocks];
+  __shared__ unsigned long long s_kept;
+  __shared__ int s_total, s_done;
+  const int t = threadIdx.x;
+  const int c = t & 255, g = t >> 8;
+  const int cc = min(c, col_blocks - 1);  // clamped column (masked later)
+  if (t < kFastColBlocks) remv[t] = 0ull;
+  if (t == 0) { s_total = 0; s_done = 0; s_kept = 0ull; }
+
+  unsigned long long r0[16], r1[16], r2[16];
+  unsigned long long d0 = 0ull, d1 = 0ull, d2 = 0ull;
+  // 32-bit byte offsets from the uniform base (n * col_blocks * 8 <= 32 MiB): one VGPR
+  // per address, so the three buffers fit the 128-VGPR budget of a 1024-thread group
+  const char* mbase = reinterpret_cast<const char*>(mask);
+  auto load_rows = [&](int b, unsigned long long (&r)[16], unsigned long long& d) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const unsigned row = (unsigned)min(b * 64 + g * 16 + j, n - 1);
+      r[j] = *reinterpret_cast<const unsigned long long*>(
+          mbase + (row * (unsigned)col_blocks + (unsigned)cc) * 8u);
+    }
+    if (t < 64) d = diag_t[min(b, col_blocks - 1) * 64 + t];
+  };
+  load_rows(0, r0, d0);
+  load_rows(min(1, col_blocks - 1), r1, d1);
+  __syncthreads();
+
+  // One block of the scan; `cur` holds block b's rows, `ahead` receives block b+2's.
+  // Unrolled x3 below so the three register buffers never move (a copy of a register
+  // with a load in flight would wait for that load).
+  auto step = [&](int b, const unsigned long long (&cur)[16], unsigned long long dcur,
+                  unsigned long long (&ahead)[16], unsigned long long& dahead) -> bool {
+    load_rows(min(b + 2, col_blocks - 1), ahead, dahead);
+    if (t < 64) {  // wave 0: resolve block b
+      const int valid = min(n - b * 64, 64);
+      const unsigned long long vmask = valid == 64 ? ~0ull : ((1ull << valid) - 1ull);
+      const int total = s_total;
+      const int room = (max_keep > 0) ? (max_keep - total) : 0x7fffffff;
+      const unsigned long long cand = ~remv[b] & vmask;
+      unsigned long long kept = cand;
+      for (int it = 0; it < 64; ++it) {
+        const unsigned long long nx = cand & __ballot((dcur & kept) == 0ull);
+        if (nx == kept) break;
+        kept = nx;
+      }
+      int kc = __popcll(kept);
+      if (kc > room) {  // the sequential scan stops at the room-th survivor
+        unsigned long long k2 = 0ull;
+        for (int r = 0; r < room; ++r) {
+          const unsigned long long low = kept & ~k2;
+          k2 |= low & (~low + 1ull);
+        }
+        kept = k2;
+        kc = room;
+      }
+      if ((kept >> t) & 1ull)
+        keep[total + __popcll(kept & ((1ull << t) - 1ull))] = b * 64 + t;
+      if (t == 0) {
+        s_kept = kept;
+        s_total = total + kc;
+        if (max_keep > 0 && total + kc >= max_keep) s_done = 1;
+      }
+    }
+    __syncthreads();
+    if (s_done) return true;
+    const unsigned long long kept = s_kept;
+    const unsigned kg = (unsigned)(kept >> (g * 16)) & 0xffffu;
+    if (kg && c > b && c < col_blocks) {
+      unsigned long long v = 0ull;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v |= ((kg >> j) & 1u) ? cur[j] : 0ull;
+      if (v) atomicOr(&remv[c], v);
+    }
+    __syncthreads();
+    return false;
+  };
+  for (int b = 0; b < col_blocks; b += 3) {
+    if (step(b, r0, d0, r2, d2) || b + 1 >= col_blocks) break;
+    if (step(b + 1, r1, d1, r0, d0) || b + 2 >= col_blocks) break;
+    if (step(b + 2, r2, d2, r1, d1)) break;
+  }
+  if (t == 0) *num_keep = s_total;
+}
+
+// General scan (n <= 131072).  One workgroup.  remv[] (removal bits per 64-box block) lives in LDS.  Block b's
 // survivors are resolved by wave 0 with the in-block (diagonal) mask words, then all
 // 16 waves OR the survivors' rows into remv for the later blocks.
 __global__ void __launch_bounds__(kScanThreads) nms_scan_kernel(
@@ -121,7 +229,7 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_kernel(
 
 size_t nms_ws_bytes(int n) {
   const int cb = div_up(n > 0 ? n : 1, 64);
-  return align_up((size_t)n * cb * sizeof(unsigned long long), 256);
+  return (align_up((size_t)n * cb, 32) + (size_t)cb * 64) * sizeof(unsigned long long);
 }
 
 int nms_launch(const float* boxes, int n, int dim, float thresh, int max_keep, int32_t* keep,
@@ -138,11 +246,16 @@ int nms_launch(const float* boxes, int n, int dim, float thresh, int max_keep, i
     return kWorkspace;
   }
   auto* mask = static_cast<unsigned long long*>(ws);
+  auto* diag_t = mask + align_up((size_t)n * cb, 32);
   hipLaunchKernelGGL(nms_mask_kernel, dim3(cb, cb), dim3(64), 0, s, boxes, n, dim, thresh,
-                     mask, cb);
+                     mask, diag_t, cb);
   TLOD_LAUNCH_CHECK();
-  hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, mask, n, cb,
-                     max_keep, keep, num_keep);
+  if (cb <= kFastColBlocks)
+    hipLaunchKernelGGL(nms_scan_fast_kernel, dim3(1), dim3(kScanThreads), 0, s, mask, diag_t, n,
+                       cb, max_keep, keep, num_keep);
+  else
+    hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, mask, n, cb,
+                       max_keep, keep, num_keep);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

@@ -83,6 +83,8 @@ SIGNATURES = {
                                     c_size_t, P]),
     "tlod_relu_bwd_bias_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, P]),
     "tlod_sgd_clip_f32": (c_int, [P, c_int, c_float, c_float, P, P, P]),
+    "tlod_space_to_depth_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_depth_to_space_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
 }
 
 _lib = None

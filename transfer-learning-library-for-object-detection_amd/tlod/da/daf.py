@@ -225,6 +225,16 @@ class _fasterRCNN(nn.Module):
                 RCNN_loss_bbox, rois_label, DA_img_loss_cls, DA_ins_loss_cls, tgt_DA_img_loss_cls,
                 tgt_DA_ins_loss_cls, DA_cst_loss, tgt_DA_cst_loss)
 
+    @staticmethod
+    def total_loss(out, lamda=0.1):
+        """methods/DAF/DAF_train.py:397-400."""
+        (_, _, _, rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, _, DA_img, DA_ins,
+         tgt_DA_img, tgt_DA_ins, DA_cst, tgt_DA_cst) = out
+        return (rpn_loss_cls.mean() + rpn_loss_box.mean() + RCNN_loss_cls.mean()
+                + RCNN_loss_bbox.mean()
+                + lamda * (DA_img.mean() + DA_ins.mean() + tgt_DA_img.mean() + tgt_DA_ins.mean()
+                           + DA_cst.mean() + tgt_DA_cst.mean()))
+
     def _init_weights(self):
         """faster_rcnn.py:227-243 (normal_init, truncated=False)."""
         def normal_init(m, mean, std):

@@ -17,13 +17,29 @@ CITYSCAPES_CLASSES = ("__background__", "bus", "bicycle", "car", "motorcycle", "
                       "rider", "train", "truck")  # lib/datasets/cityscape.py:51-54
 
 
-def build_daf_vgg16(device, classes=CITYSCAPES_CLASSES, seed=0):
-    from ..da.daf import vgg16
-    setup_training_cfg("vgg16")
+METHODS = ("daf", "maf")
+
+
+def build_model(method, device, net="vgg16", classes=CITYSCAPES_CLASSES, seed=0):
+    """<method>.vgg16(classes).create_architecture() (methods/<M>/<M>_train.py), random
+    init (the pretrained caffe weights are external downloads)."""
+    if method == "daf":
+        from ..da.daf import vgg16
+    elif method == "maf":
+        from ..da.maf import vgg16
+    else:
+        raise ValueError(f"unknown method {method!r} (have {METHODS})")
+    if net != "vgg16":
+        raise NotImplementedError(f"backbone {net!r}")
+    setup_training_cfg(net)
     torch.manual_seed(seed)
     m = vgg16(classes, pretrained=False, class_agnostic=False)
     m.create_architecture()
     return m.to(device).train()
+
+
+def build_daf_vgg16(device, classes=CITYSCAPES_CLASSES, seed=0):
+    return build_model("daf", device, "vgg16", classes, seed)
 
 
 def make_optimizer(model, lr, momentum=None, weight_decay=None, double_bias=None, bias_decay=None,
@@ -103,22 +119,19 @@ class SyntheticCityscapes:
 
 
 def daf_loss(out, lamda=0.1):
-    (_, _, _, rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, _, DA_img, DA_ins,
-     tgt_DA_img, tgt_DA_ins, DA_cst, tgt_DA_cst) = out
-    return (rpn_loss_cls.mean() + rpn_loss_box.mean() + RCNN_loss_cls.mean()
-            + RCNN_loss_bbox.mean()
-            + lamda * (DA_img.mean() + DA_ins.mean() + tgt_DA_img.mean() + tgt_DA_ins.mean()
-                       + DA_cst.mean() + tgt_DA_cst.mean()))
+    from ..da.daf import _fasterRCNN
+    return _fasterRCNN.total_loss(out, lamda)
 
 
 def train_step(model, optimizer, batch, lamda=0.1, clip=10.0, reducer=None):
-    """One DAF iteration; returns the loss as a device tensor (no host sync)."""
+    """One DAF/MAF iteration (the method's own loss sum, model.total_loss); returns the
+    loss as a device tensor (no host sync)."""
     if reducer is not None:
         reducer.zero_grad()  # grads are views into the reducer's flat buckets
     else:
         optimizer.zero_grad(set_to_none=True)
     out = model(*batch)
-    loss = daf_loss(out, lamda)
+    loss = model.total_loss(out, lamda)
     loss.backward()
     if reducer is not None:
         reducer.finish()
@@ -132,13 +145,13 @@ def train_step(model, optimizer, batch, lamda=0.1, clip=10.0, reducer=None):
     return loss.detach()
 
 
-def smoke_step(device):
-    """One tiny DAF-VGG16 forward+backward+update on `device` (used by smoke())."""
-    model = build_daf_vgg16(device)
+def smoke_step(device, method="daf"):
+    """One tiny <method>-VGG16 forward+backward+update on `device` (used by smoke())."""
+    model = build_model(method, device)
     opt = make_optimizer(model, 2e-3)
     data = SyntheticCityscapes(device, H=192, W=320, G=4, pool=1, seed=7)
     loss = train_step(model, opt, data.next())
     torch.cuda.synchronize()
     v = float(loss)
-    assert math.isfinite(v), f"non-finite DAF loss {v}"
+    assert math.isfinite(v), f"non-finite {method} loss {v}"
     return v
