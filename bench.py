@@ -39,8 +39,8 @@ def parse():
     ap.add_argument("--cpu-baseline-steps", type=int, default=2,
                     help="oracle CPU steps timed on rank 0 at N=1 (0 disables)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--method", choices=("daf", "maf"), default="daf",
-                    help="detector (the headline metric is DAF; MAF is a secondary workload)")
+    ap.add_argument("--method", choices=("daf", "maf", "atf"), default="daf",
+                    help="detector (the headline metric is DAF; MAF / ATF are secondary workloads)")
     return ap.parse_args()
 
 

@@ -37,3 +37,21 @@ def test_fused_sgd_matches_torch(clip):
         to.step()
         for pa, pb in zip(a.parameters(), b.parameters()):
             torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+
+
+def test_params_without_grad_are_skipped():
+    """torch SGD leaves a parameter whose .grad is None untouched (no weight decay); ATF
+    owns one such module (RCNN_rpn_t, lib/ATF/faster_rcnn.py:95, never called)."""
+    from tlod.optim import FusedSGDClip
+    torch.manual_seed(0)
+    used, unused = torch.nn.Linear(8, 8).cuda(), torch.nn.Linear(8, 8).cuda()
+    before = [p.detach().clone() for p in unused.parameters()]
+    params = list(used.parameters()) + list(unused.parameters())
+    opt = FusedSGDClip([{"params": params, "lr": 0.1, "weight_decay": 5e-4}], clip_norm=10.0)
+    for _ in range(2):
+        opt.zero_grad()
+        used(torch.randn(4, 8, device="cuda")).sum().backward()
+        opt.step()
+    for p, b in zip(unused.parameters(), before):
+        assert torch.equal(p.detach(), b)
+    assert all(p.grad is None for p in unused.parameters())

@@ -1,0 +1,214 @@
+"""ATF (lib/ATF/{faster_rcnn,vgg16,rpn}.py) on the tlod kernels.
+
+``vgg16(classes).create_architecture()`` then ``model(im_data, im_info, gt_boxes,
+num_boxes, need_backprop, tgt_im_data, tgt_im_info, tgt_gt_boxes, tgt_num_boxes,
+tgt_need_backprop)`` returns the reference's 12-tuple (lib/ATF/faster_rcnn.py:362-363;
+note the order: DA_img, tgt_DA_img, DA_ins, tgt_DA_ins).
+
+ATF keeps two copies of conv3_1..conv5_3: ``RCNN_base`` (the "s" branch) and
+``RCNN_base_t`` (deep copies of layers 10+, sharing the frozen conv1/conv2, vgg16.py:
+44-64).  Per step the source image runs through both branches, each with its own RPN
+losses (the same RCNN_rpn, train mode) and proposal-target sampling; the detection losses
+sum over the branches; the source-domain discriminators see the t branch (conv3/4/5 and
+the 2000 t-branch proposals through fc6/fc7); the target image runs the s branch with the
+RPN in eval mode and TEST post-NMS top-N set to the train count (:259-260).
+
+Scheduling (same math as the reference, fewer passes): conv1/conv2 run once for both
+images (frozen, shared); the s branch runs source+target batched; the three RPN heads
+(s/src, t/src, s/tgt) run as one batch; the four RoI sets (s sampled, t sampled, t
+proposals, target proposals) go through one RoIAlign and one fc6/fc7 pass.  The
+reference's unused work — RoIAlign of the s-branch proposals (:185-199) and the target
+cls_score (:295-296) — is skipped; it does not feed any output.
+"""
+import copy
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..config import cfg
+from ..detector.losses import smooth_l1_loss
+from ..rpn.rpn_head import _RPN
+from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, image_label
+from .daf import vgg16 as _daf_vgg16
+
+
+def instance_label_f(n_rows, need_backprop, minibatch=256):
+    """ATF InstanceLabelResizeLayer (lib/ATF/LabelResizeLayer.py:50-60): float zeros, then
+    rows [i*256, (i+1)*256) := need_backprop[i]."""
+    nb = need_backprop.view(-1).float()
+    y = torch.zeros((n_rows, 1), dtype=torch.float32, device=nb.device)
+    for i in range(nb.numel()):
+        y[i * minibatch:(i + 1) * minibatch] = nb[i]
+    return y
+
+
+class _fasterRCNN(_DAFBase):
+    """lib/ATF/faster_rcnn.py:84-389."""
+
+    def __init__(self, classes, class_agnostic):
+        super().__init__(classes, class_agnostic)
+        del self.consistency_loss
+        # RCNN_rpn_t is built by the reference (:95) but never called: it keeps its init
+        # weights (SGD skips parameters without gradients) — frozen here to the same effect
+        self.RCNN_rpn_t = _RPN(self.dout_base_model)
+        for p in self.RCNN_rpn_t.parameters():
+            p.requires_grad = False
+        self.RCNN_imageDA_3 = _ImageDA(256)
+        self.RCNN_imageDA_4 = _ImageDA(512)
+        self.RCNN_imageDA = _ImageDA(self.dout_base_model)
+        self.RCNN_instanceDA = _InstanceDA(self.instance_dim)
+
+    def _branch(self, layers, z):
+        c3 = layers[10:16](z)
+        c4 = layers[16:23](c3)
+        return c3, c4, layers[23:](c4)
+
+    @staticmethod
+    def _img_loss(score, need):
+        return F.nll_loss(F.log_softmax(score, 1), image_label(score, need), ignore_index=-1)
+
+    def _sampled(self, rois, gt_boxes, num_boxes):
+        rois, label, target, inside, outside = self.RCNN_proposal_target(
+            rois, gt_boxes, num_boxes, rng=self.replay_rng)
+        return (rois, label.view(-1).long(), target.view(-1, target.size(2)),
+                inside.view(-1, inside.size(2)), outside.view(-1, outside.size(2)))
+
+    def forward(self, im_data, im_info, gt_boxes, num_boxes, need_backprop,
+                tgt_im_data, tgt_im_info, tgt_gt_boxes, tgt_num_boxes, tgt_need_backprop):
+        batch_size = im_data.size(0)
+        im_info = im_info.detach()
+        gt_boxes = gt_boxes.detach()
+        same = (im_data.shape == tgt_im_data.shape) and batch_size == 1
+        rpn = self.RCNN_rpn
+
+        # ---- backbones: frozen conv1/conv2 are shared by both branches (vgg16.py:46-47)
+        if same:
+            z = self.RCNN_base[:10](torch.cat([im_data, tgt_im_data], 0))
+            c3s, c4s, bs = self._branch(self.RCNN_base, z)
+            c3_t, c4_t, base_t = self._branch(self.RCNN_base_t, z[:1])
+            base_feat, tgt_base_feat = bs[:1], bs[1:]
+            tgt_c3, tgt_c4 = c3s[1:], c4s[1:]
+            heads = rpn.head(torch.cat([base_feat, base_t, tgt_base_feat], 0))
+            hs = [tuple(h[i:i + 1] for h in heads) for i in range(3)]
+        else:
+            z = self.RCNN_base[:10](im_data)
+            _, _, base_feat = self._branch(self.RCNN_base, z)
+            c3_t, c4_t, base_t = self._branch(self.RCNN_base_t, z)
+            tgt_c3, tgt_c4, tgt_base_feat = self._branch(self.RCNN_base,
+                                                         self.RCNN_base[:10](tgt_im_data))
+            hs = [rpn.head(f) for f in (base_feat, base_t, tgt_base_feat)]
+
+        # ---- RPN, train mode, on the source image through both branches (:130-134)
+        rois_domain = rpn.RPN_proposal((hs[0][2].detach(), hs[0][3].detach(), im_info, "TRAIN"))
+        l_cls1, l_box1, _ = rpn.losses(hs[0][0], hs[0][1], hs[0][3], gt_boxes, im_info, num_boxes,
+                                       rng=self.replay_rng)
+        rois_domain_t = rpn.RPN_proposal((hs[1][2].detach(), hs[1][3].detach(), im_info, "TRAIN"))
+        l_cls2, l_box2, _ = rpn.losses(hs[1][0], hs[1][1], hs[1][3], gt_boxes, im_info, num_boxes,
+                                       rng=self.replay_rng)
+        rpn_loss_cls = l_cls1 + l_cls2
+        rpn_loss_bbox = l_box1 + l_box2
+        # target image: eval-mode RPN with TEST post-NMS top-N := train count (:258-260)
+        cfg.TEST.RPN_POST_NMS_TOP_N = rois_domain.size(1)
+        tgt_rois = rpn.RPN_proposal((hs[2][2].detach(), hs[2][3].detach(),
+                                     tgt_im_info.detach(), "TEST"))
+        if self.capture is not None:
+            self.capture.update(s_rois=rois_domain.detach().clone(),
+                                st_rois=rois_domain_t.detach().clone(),
+                                t_rois=tgt_rois.detach().clone())
+
+        rois, rois_label, rois_target, rois_inside_ws, rois_outside_ws = \
+            self._sampled(rois_domain, gt_boxes, num_boxes)
+        rois_t, rois_label_t, rois_target_t, rois_inside_ws_t, rois_outside_ws_t = \
+            self._sampled(rois_domain_t, gt_boxes, num_boxes)
+
+        # ---- one RoIAlign + fc6/fc7 pass over the four RoI sets
+        sets = (rois, rois_t, rois_domain_t, tgt_rois)
+        n = [r.size(1) for r in sets]
+        if same:
+            feats = torch.cat([base_feat, tgt_base_feat, base_t], 0)
+            idx = (0, 2, 2, 1)
+            rr = []
+            for r, i in zip(sets, idx):
+                r = r.view(-1, 5).clone()
+                r[:, 0] = float(i)
+                rr.append(r)
+            fc7 = self._head_to_tail(self._pool(feats, torch.cat(rr, 0)))
+        else:
+            maps = (base_feat, base_t, base_t, tgt_base_feat)
+            fc7 = torch.cat([self._head_to_tail(self._pool(f, r.view(-1, 5)))
+                             for f, r in zip(maps, sets)], 0)
+        o = [0]
+        for k in n:
+            o.append(o[-1] + k)
+        det = fc7[:o[2]]  # s-branch and t-branch sampled RoIs
+
+        bbox_all = self.RCNN_bbox_pred(det)
+        labels = torch.cat([rois_label, rois_label_t])
+        if self.training and not self.class_agnostic:
+            view = bbox_all.view(bbox_all.size(0), int(bbox_all.size(1) / 4), 4)
+            bbox_all = torch.gather(view, 1, labels.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
+        cls_all = self.RCNN_cls_score(det)
+        RCNN_loss_cls = (F.cross_entropy(cls_all[:n[0]], rois_label)
+                         + F.cross_entropy(cls_all[n[0]:], rois_label_t))
+        RCNN_loss_bbox = (smooth_l1_loss(bbox_all[:n[0]], rois_target, rois_inside_ws,
+                                         rois_outside_ws)
+                          + smooth_l1_loss(bbox_all[n[0]:], rois_target_t, rois_inside_ws_t,
+                                           rois_outside_ws_t))
+        cls_prob = F.softmax(cls_all[:n[0]], 1).view(batch_size, rois_t.size(1), -1)
+        bbox_pred = bbox_all[:n[0]].view(batch_size, rois_t.size(1), -1)
+
+        # ---- image DA: source through the t branch, target through the s branch (:306-354)
+        da_heads = (self.RCNN_imageDA_3, self.RCNN_imageDA_4, self.RCNN_imageDA)
+        if same:
+            pairs = ((c3_t, tgt_c3), (c4_t, tgt_c4), (base_t, tgt_base_feat))
+            sc = [h(torch.cat(p, 0), need_backprop.new_ones(2))[0] for h, p in zip(da_heads, pairs)]
+            s_scores, t_scores = [s[:1] for s in sc], [s[1:] for s in sc]
+        else:
+            s_scores = [h(f, need_backprop)[0] for h, f in zip(da_heads, (c3_t, c4_t, base_t))]
+            t_scores = [h(f, tgt_need_backprop)[0]
+                        for h, f in zip(da_heads, (tgt_c3, tgt_c4, tgt_base_feat))]
+        DA_img_loss_cls = sum(self._img_loss(s, need_backprop) for s in s_scores)
+        tgt_DA_img_loss_cls = sum(self._img_loss(s, tgt_need_backprop) for s in t_scores)
+
+        # ---- instance DA: t-branch proposals (source) and target proposals (:326-345)
+        ins, _ = self.RCNN_instanceDA(fc7[o[2]:], need_backprop.new_ones(1))
+        ins_s, ins_t = ins[:n[2]], ins[n[2]:]
+        DA_ins_loss_cls = F.binary_cross_entropy(ins_s, instance_label_f(n[2], need_backprop))
+        tgt_DA_ins_loss_cls = F.binary_cross_entropy(ins_t, instance_label_f(n[3], tgt_need_backprop))
+        return (rois_t, cls_prob, bbox_pred, rpn_loss_cls, rpn_loss_bbox, RCNN_loss_cls,
+                RCNN_loss_bbox, rois_label_t, DA_img_loss_cls, tgt_DA_img_loss_cls,
+                DA_ins_loss_cls, tgt_DA_ins_loss_cls)
+
+    @staticmethod
+    def total_loss(out, lamda=0.1):
+        """methods/ATF/ATF_train.py:405-408 (image DA weighted 7x)."""
+        (_, _, _, rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, _, DA_img,
+         tgt_DA_img, DA_ins, tgt_DA_ins) = out
+        return (rpn_loss_cls.mean() + rpn_loss_box.mean() + RCNN_loss_cls.mean()
+                + RCNN_loss_bbox.mean()
+                + lamda * (7 * DA_img.mean() + DA_ins.mean() + 7 * tgt_DA_img.mean()
+                           + tgt_DA_ins.mean()))
+
+
+class vgg16(_fasterRCNN):
+    """lib/ATF/vgg16.py:20-79."""
+
+    def __init__(self, classes, pretrained=False, class_agnostic=False):
+        self.dout_base_model = 512
+        self.instance_dim = 4096
+        self.pretrained = pretrained
+        self.class_agnostic = class_agnostic
+        _fasterRCNN.__init__(self, classes, class_agnostic)
+
+    def _init_modules(self):
+        _daf_vgg16._init_modules(self)
+        layers = list(self.RCNN_base)
+        self.RCNN_base_t = nn.Sequential(*(layers[:10] + [copy.deepcopy(m) for m in layers[10:]]))
+        lt = list(self.RCNN_base_t)
+        self.conv3_s, self.conv3_t = nn.Sequential(*layers[:16]), nn.Sequential(*lt[:16])
+        self.conv34_s, self.conv34_t = nn.Sequential(*layers[16:23]), nn.Sequential(*lt[16:23])
+        self.conv45_s, self.conv45_t = nn.Sequential(*layers[23:]), nn.Sequential(*lt[23:])
+
+    def _head_to_tail(self, pool5):
+        return self.RCNN_top(pool5.view(pool5.size(0), -1))

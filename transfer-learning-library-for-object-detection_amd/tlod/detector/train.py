@@ -17,7 +17,7 @@ CITYSCAPES_CLASSES = ("__background__", "bus", "bicycle", "car", "motorcycle", "
                       "rider", "train", "truck")  # lib/datasets/cityscape.py:51-54
 
 
-METHODS = ("daf", "maf")
+METHODS = ("daf", "maf", "atf")
 
 
 def build_model(method, device, net="vgg16", classes=CITYSCAPES_CLASSES, seed=0):
@@ -27,6 +27,8 @@ def build_model(method, device, net="vgg16", classes=CITYSCAPES_CLASSES, seed=0)
         from ..da.daf import vgg16
     elif method == "maf":
         from ..da.maf import vgg16
+    elif method == "atf":
+        from ..da.atf import vgg16
     else:
         raise ValueError(f"unknown method {method!r} (have {METHODS})")
     if net != "vgg16":
@@ -124,7 +126,7 @@ def daf_loss(out, lamda=0.1):
 
 
 def train_step(model, optimizer, batch, lamda=0.1, clip=10.0, reducer=None):
-    """One DAF/MAF iteration (the method's own loss sum, model.total_loss); returns the
+    """One DAF/MAF/ATF iteration (the method's own loss sum, model.total_loss); returns the
     loss as a device tensor (no host sync)."""
     if reducer is not None:
         reducer.zero_grad()  # grads are views into the reducer's flat buckets

@@ -43,8 +43,11 @@ class FusedSGDClip:
                 p.grad.zero_()
 
     def _chunk_table(self):
+        """Descriptor rows for every parameter that has a gradient (torch.optim.SGD skips
+        the others entirely: no weight decay, no momentum update)."""
         grads = [p.grad for p in self.params]
-        key = tuple(g.data_ptr() for g in grads) + tuple(g["lr"] for g in self.param_groups)
+        key = tuple(0 if g is None else g.data_ptr() for g in grads) + \
+            tuple(g["lr"] for g in self.param_groups)
         if key == self._key:
             return self._table
         rows = []
@@ -52,6 +55,9 @@ class FusedSGDClip:
         for g in self.param_groups:
             for p in g["params"]:
                 gr, buf = p.grad, self.bufs[idx]
+                if gr is None:
+                    idx += 1
+                    continue
                 assert gr.is_contiguous() and p.is_contiguous()
                 n = p.numel()
                 for off in range(0, n, CHUNK):
@@ -69,10 +75,9 @@ class FusedSGDClip:
 
     @torch.no_grad()
     def step(self):
-        for p in self.params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
         table = self._chunk_table()
+        if self._n == 0:
+            return self.norm_scale[0]
         _lib.check(_lib.lib().tlod_sgd_clip_f32(
             _lib.ptr(table), self._n, self.momentum, self.clip_norm, _lib.ptr(self.partials),
             _lib.ptr(self.norm_scale), _lib.stream_of(self.partials)), "sgd_clip")
