@@ -203,7 +203,13 @@ int tlod_proposal_target_f32(const float* rois, int B, int R, const float* gt_bo
  * the output tiles cannot fill the chip; *_workspace_bytes reports the slab size (0 when no
  * split is used).
  * relu_bwd_bias: g = dy * (y > 0) (y may be NULL: g = dy), db += sum over n,h,w of g
- *        (db may be NULL).  g may alias dy. */
+ *        (db may be NULL).  g may alias dy.
+ * fwd_ex: y = act(conv * scale[co] + bias[co] + residual) — the ResNet bottleneck epilogue
+ *        (frozen BatchNorm folded to scale/bias, lib/DAF/resnet.py:261-284; identity or
+ *        downsample branch added before the ReLU, resnet.py:94-97).  Any of scale, bias,
+ *        residual may be NULL; residual (N,Cout,H,W) must not alias y.
+ * relu_bwd_ex: g0 = dy * (y > 0); g = g0 * scale[c] (scale may be NULL); g_raw = g0 when
+ *        g_raw != NULL (the residual branch's gradient); db += sum g0 when db != NULL. */
 int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
                            tlod_stream_t stream);
 int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, int KS, float* wd,
@@ -221,6 +227,27 @@ int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, int accumula
                         tlod_stream_t stream);
 int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db, int N, int C,
                            int HW, tlod_stream_t stream);
+int tlod_conv_fwd_ex_f32(const float* x, const float* wk, const float* scale, const float* bias,
+                         const float* residual, float* y, int N, int Cin, int H, int W, int Cout,
+                         int KS, int relu, void* ws, size_t ws_bytes, tlod_stream_t stream);
+int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float* scale, float* g,
+                         float* g_raw, float* db, int N, int C, int HW, tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ ResNet101 extras
+ * Replaces: cuDNN for the ResNet101 stem conv1 7x7/2 + bn1 + relu (lib/DAF/resnet.py:107-110,
+ *   frozen, forward only) and the stride-2 1x1 convolutions of the caffe-style bottleneck
+ *   (resnet.py:71 conv1 stride, :133-135 downsample).
+ * stem: x (N,3,H,W) -> y (N,64,Ho,Wo), Ho = (H-1)/2+1; weight (64,3,7,7); y = act(conv *
+ *   scale + bias) (scale/bias: folded bn1, may be NULL).
+ * subsample2: y = x[:, :, ::2, ::2]  (N,C,(H+1)/2,(W+1)/2) — a stride-2 1x1 conv is the
+ *   stride-1 conv of this; upsample2_zero is its adjoint (dx (N,C,H,W), zeros off-grid). */
+int tlod_stem_conv7x7s2_f32(const float* x, const float* weight, const float* scale,
+                            const float* bias, float* y, int N, int H, int W, int relu,
+                            tlod_stream_t stream);
+int tlod_subsample2_f32(const float* x, int N, int C, int H, int W, float* y,
+                        tlod_stream_t stream);
+int tlod_upsample2_zero_f32(const float* dy, int N, int C, int H, int W, float* dx,
+                            tlod_stream_t stream);
 
 
 /* ------------------------------------------------------------------ Optimiser step

@@ -59,34 +59,46 @@ def _smooth_l1(pred, target, iw, ow, sigma=1.0, dim=(1,)):
 
 
 class OracleDAF(nn.Module):
-    def __init__(self, n_classes=9, dropout=0.5):
+    """backbone "vgg16" (lib/DAF/vgg16.py) or "res101" (lib/DAF/resnet.py, oracle.resnet;
+    RoI batch 128 from cfgs/res101.yml, instance head on the 2048-d features)."""
+
+    def __init__(self, n_classes=9, dropout=0.5, backbone="vgg16"):
         super().__init__()
-        layers, cin = [], 3
-        for v in VGG16_CFG:
-            if v == "M":
-                layers.append(nn.MaxPool2d(2, 2))
-            else:
-                layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
-                cin = v
-        self.RCNN_base = nn.Sequential(*layers)
-        for i in range(10):
-            for p in self.RCNN_base[i].parameters():
-                p.requires_grad = False
-        self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), nn.ReLU(True), nn.Dropout(dropout),
-                                      nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout))
-        self.RCNN_cls_score = nn.Linear(4096, n_classes)
-        self.RCNN_bbox_pred = nn.Linear(4096, 4 * n_classes)
+        self.backbone = backbone
+        self.rcnn_cfg = dict(orpn.DEFAULT_RCNN)
+        if backbone == "vgg16":
+            layers, cin = [], 3
+            for v in VGG16_CFG:
+                if v == "M":
+                    layers.append(nn.MaxPool2d(2, 2))
+                else:
+                    layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
+                    cin = v
+            self.RCNN_base = nn.Sequential(*layers)
+            for i in range(10):
+                for p in self.RCNN_base[i].parameters():
+                    p.requires_grad = False
+            self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), nn.ReLU(True), nn.Dropout(dropout),
+                                          nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout))
+            din, dfeat = 512, 4096
+        else:
+            from .resnet import resnet101_parts
+            self.RCNN_base, self.RCNN_top = resnet101_parts()
+            self.rcnn_cfg["batch"] = 128
+            din, dfeat = 1024, 2048
+        self.RCNN_cls_score = nn.Linear(dfeat, n_classes)
+        self.RCNN_bbox_pred = nn.Linear(dfeat, 4 * n_classes)
         rpn = nn.Module()
-        rpn.RPN_Conv = nn.Conv2d(512, 512, 3, padding=1)
+        rpn.RPN_Conv = nn.Conv2d(din, 512, 3, padding=1)
         rpn.RPN_cls_score = nn.Conv2d(512, 24, 1)
         rpn.RPN_bbox_pred = nn.Conv2d(512, 48, 1)
         self.RCNN_rpn = rpn
         ida = nn.Module()
-        ida.Conv1 = nn.Conv2d(512, 512, 1, bias=False)
+        ida.Conv1 = nn.Conv2d(din, 512, 1, bias=False)
         ida.Conv2 = nn.Conv2d(512, 2, 1, bias=False)
         self.RCNN_imageDA = ida
         ins = nn.Module()
-        ins.dc_ip1, ins.dc_ip2, ins.clssifer = nn.Linear(4096, 1024), nn.Linear(1024, 1024), nn.Linear(1024, 1)
+        ins.dc_ip1, ins.dc_ip2, ins.clssifer = nn.Linear(dfeat, 1024), nn.Linear(1024, 1024), nn.Linear(1024, 1)
         self.RCNN_instanceDA = ins
         self.dropout = dropout
         self.base_anchors = orpn.make_base_anchors(CFG["scales"], CFG["ratios"])
@@ -110,9 +122,23 @@ class OracleDAF(nn.Module):
         x = F.dropout(F.relu(m.dc_ip2(x)), self.dropout, self.training)
         return torch.sigmoid(m.clssifer(x))
 
+    def train(self, mode=True):
+        super().train(mode)
+        if self.backbone == "res101":  # resnet.py:269-284
+            from .resnet import bn_eval
+            bn_eval(self)
+        return self
+
+    def _head_to_tail(self, pooled):
+        if self.backbone == "res101":
+            return self.RCNN_top(pooled).mean(3).mean(2)  # resnet.py:286-288
+        return self.RCNN_top(pooled.view(pooled.size(0), -1))
+
     def _backbone(self, im):
         """RCNN_base in the three pieces MAF taps (lib/MAF/vgg16.py:84-86): conv3 =
         features[:16], conv34 = [16:23], conv45 = [23:-1]."""
+        if self.backbone == "res101":
+            return None, None, self.RCNN_base(im)
         c3 = self.RCNN_base[:16](im)
         c4 = self.RCNN_base[16:23](c3)
         return c3, c4, self.RCNN_base[23:](c4)
@@ -140,10 +166,10 @@ class OracleDAF(nn.Module):
         rpn_loss_cls = F.cross_entropy(s2[keep], lab_t[keep].long())
         rpn_loss_box = _smooth_l1(bbox, torch.from_numpy(tgt), torch.from_numpy(iw),
                                   torch.from_numpy(ow), sigma=3, dim=[1, 2, 3])
-        r, rl, rt, riw, row = orpn.proposal_target(rois, gt.numpy(), rng)
+        r, rl, rt, riw, row = orpn.proposal_target(rois, gt.numpy(), rng, self.rcnn_cfg)
         rl = torch.from_numpy(rl).view(-1).long()
         pooled = _RoIAlignAvgCPU.apply(base, torch.from_numpy(r).view(-1, 5))
-        fc7 = self.RCNN_top(pooled.view(pooled.size(0), -1))
+        fc7 = self._head_to_tail(pooled)
         bp = self.RCNN_bbox_pred(fc7).view(fc7.size(0), -1, 4)
         bp = torch.gather(bp, 1, rl.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
         cls = self.RCNN_cls_score(fc7)
@@ -159,7 +185,7 @@ class OracleDAF(nn.Module):
         if rois_override is not None:
             t_rois = rois_override[1]
         t_pooled = _RoIAlignAvgCPU.apply(t_base, torch.from_numpy(t_rois).view(-1, 5))
-        t_fc7 = self.RCNN_top(t_pooled.view(t_pooled.size(0), -1))
+        t_fc7 = self._head_to_tail(t_pooled)
         return dict(rpn_loss_cls=rpn_loss_cls, rpn_loss_box=rpn_loss_box, RCNN_loss_cls=rcnn_cls,
                     RCNN_loss_bbox=rcnn_box, rois=r, c3=c3, c4=c4, base=base, fc7=fc7, cls=cls,
                     t_c3=t_c3, t_c4=t_c4, t_base=t_base, t_fc7=t_fc7)

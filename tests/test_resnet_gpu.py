@@ -1,0 +1,189 @@
+"""ResNet101 on the device (tlod.detector.resnet) vs the torch-CPU restatement
+(oracle/resnet.py) with identical weights: the stem kernel, the stride-2 subsample pair,
+the fused conv+BN(+residual)+ReLU epilogue, whole bottlenecks (NCHW backbone path and the
+channels-last RoI-head path), and the DAF-ResNet101 training step against the oracle.
+
+Bars: permutations bit-exact; fp32 conv arithmetic normwise 1e-5 per layer (the MFMA path
+is an exact-f32 FMA chain); full-step losses 1e-4 relative, gradients normwise 1e-2
+(see tests/test_daf_step_gpu.py for why).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _close(got, ref, tol=1e-5):
+    got, ref = got.detach().double().cpu(), ref.detach().double().cpu()
+    err = float((got - ref).norm() / max(float(ref.norm()), 1e-30))
+    assert err <= tol, err
+
+
+def _rand_bn(bn, g):
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(bn.weight.shape, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(bn.bias.shape, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(bn.running_mean.shape, generator=g) * 0.1)
+        bn.running_var.copy_(torch.rand(bn.running_var.shape, generator=g) + 0.5)
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (37, 51)])
+def test_stem_conv(H, W):
+    from tlod.detector.resnet import stem
+    g = torch.Generator().manual_seed(H + W)
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+    bn = torch.nn.BatchNorm2d(64).eval()
+    _rand_bn(bn, g)
+    for p in list(conv.parameters()) + list(bn.parameters()):
+        p.requires_grad = False
+    x = torch.randn(2, 3, H, W, generator=g) * 50
+    ref = F.relu(bn(conv(x)))
+    got = stem(x.to(dev), conv.to(dev), bn.to(dev))
+    assert got.shape == ref.shape
+    _close(got, ref)
+
+
+@pytest.mark.parametrize("H,W", [(8, 10), (7, 7), (38, 75)])
+def test_subsample_pair_exact(H, W):
+    from tlod.detector.resnet import Subsample2Function
+    x = torch.randn(2, 3, H, W, device=dev, requires_grad=True)
+    y = Subsample2Function.apply(x)
+    assert torch.equal(y, x[:, :, ::2, ::2])
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    ref = torch.zeros_like(x)
+    ref[:, :, ::2, ::2] = gy
+    assert torch.equal(x.grad, ref)
+
+
+@pytest.mark.parametrize("KS,res", [(1, True), (3, False), (3, True)])
+def test_conv_bn_epilogue(KS, res):
+    from tlod.conv import ConvBNFunction
+    g = torch.Generator().manual_seed(KS * 10 + res)
+    x = torch.randn(2, 64, 19, 37, generator=g)
+    w = torch.randn(128, 64, KS, KS, generator=g) * 0.05
+    sc, sh = torch.rand(128, generator=g) + 0.5, torch.randn(128, generator=g)
+    r = torch.randn(2, 128, 19, 37, generator=g) if res else None
+    xd, wd = x.to(dev).requires_grad_(True), w.to(dev).requires_grad_(True)
+    rd = r.to(dev).requires_grad_(True) if res else None
+    y = ConvBNFunction.apply(xd, wd, sc.to(dev), sh.to(dev), rd, True)
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    rr = r.double().requires_grad_(True) if res else None
+    pre = F.conv2d(xr, wr, padding=KS // 2) * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1)
+    if res:
+        pre = pre + rr
+    _close(y, F.relu(pre))
+    yr = pre * (y.detach().cpu() > 0).double()  # backward through the device's mask
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy.to(dev))
+    yr.backward(gy.double())
+    _close(xd.grad, xr.grad)
+    _close(wd.grad, wr.grad)
+    if res:
+        _close(rd.grad, rr.grad)
+
+
+def _pair_blocks(inplanes, planes, stride, seed):
+    from oracle.resnet import Bottleneck as OB
+    from tlod.detector.resnet import Bottleneck
+    g = torch.Generator().manual_seed(seed)
+    ds = None
+    if stride != 1 or inplanes != planes * 4:
+        ds = torch.nn.Sequential(torch.nn.Conv2d(inplanes, planes * 4, 1, stride, bias=False),
+                                 torch.nn.BatchNorm2d(planes * 4))
+    ob = OB(inplanes, planes, stride, ds).eval()
+    for m in ob.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            _rand_bn(m, g)
+            for p in m.parameters():
+                p.requires_grad = False
+        elif isinstance(m, torch.nn.Conv2d):
+            with torch.no_grad():
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * (2.0 / m.weight[0].numel()) ** 0.5)
+    ds2 = None
+    if ds is not None:
+        ds2 = torch.nn.Sequential(torch.nn.Conv2d(inplanes, planes * 4, 1, stride, bias=False),
+                                  torch.nn.BatchNorm2d(planes * 4))
+    db = Bottleneck(inplanes, planes, stride, ds2)
+    db.load_state_dict(ob.state_dict())
+    for m in db.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            for p in m.parameters():
+                p.requires_grad = False
+    return ob, db.to(dev).eval(), g
+
+
+@pytest.mark.parametrize("inplanes,planes,stride,H,W", [(256, 64, 1, 20, 36), (256, 128, 2, 19, 37),
+                                                        (512, 128, 1, 10, 19)])
+def test_bottleneck_nchw(inplanes, planes, stride, H, W):
+    ob, db, g = _pair_blocks(inplanes, planes, stride, inplanes + planes + stride)
+    x = torch.randn(2, inplanes, H, W, generator=g)
+    xd = x.to(dev).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y, yr = db(xd), ob(xr)
+    _close(y, yr, 1e-5)
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy.to(dev))
+    yr.backward(gy)
+    _close(xd.grad, xr.grad, 1e-4)
+    for (k, p), (_, q) in zip(db.named_parameters(), ob.named_parameters()):
+        if q.requires_grad:
+            _close(p.grad, q.grad, 1e-4)
+
+
+@pytest.mark.parametrize("inplanes,planes,stride,R", [(1024, 512, 2, 6), (2048, 512, 1, 5)])
+def test_bottleneck_head_nhwc(inplanes, planes, stride, R):
+    ob, db, g = _pair_blocks(inplanes, planes, stride, R)
+    H = 7 if stride == 2 else 4
+    x = torch.randn(R, inplanes, H, H, generator=g)
+    xd = x.to(dev).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y = db.forward_nhwc(xd.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+    yr = ob(xr)
+    _close(y, yr, 1e-5)
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy.to(dev))
+    yr.backward(gy)
+    _close(xd.grad, xr.grad, 1e-4)
+
+
+LOSSES = ["rpn_loss_cls", "rpn_loss_box", "RCNN_loss_cls", "RCNN_loss_bbox", "DA_img_loss_cls",
+          "DA_ins_loss_cls", "tgt_DA_img_loss_cls", "tgt_DA_ins_loss_cls", "DA_cst_loss",
+          "tgt_DA_cst_loss"]
+IDX = [3, 4, 5, 6, 8, 9, 10, 11, 12, 13]
+
+
+def test_daf_resnet101_step_matches_oracle():
+    from oracle.daf_step import OracleDAF, synthetic_batch, total_loss
+    from tlod.detector.train import build_model
+    m = build_model("daf", dev, net="res101", seed=5)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    o = OracleDAF(dropout=0.0, backbone="res101").train()
+    o.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=True)
+    cpu_batch = synthetic_batch(224, 320, seed=6)
+    gpu_batch = tuple(t.to(dev) for t in cpu_batch)
+    m.replay_rng = np.random.RandomState(3)
+    m.capture = {}
+    out = m(*gpu_batch)
+    m.total_loss(out).backward()
+    assert out[0].shape[1] == 128  # cfgs/res101.yml TRAIN.BATCH_SIZE
+    ref = o(cpu_batch, np.random.RandomState(3),
+            rois_override=(m.capture["s_rois"].cpu().numpy(), m.capture["t_rois"].cpu().numpy()))
+    total_loss(ref).backward()
+    for name, i in zip(LOSSES, IDX):
+        gv, r = float(out[i].detach()), float(ref[name].detach())
+        assert abs(gv - r) <= 1e-4 * max(abs(r), 1e-3), (name, gv, r)
+    np.testing.assert_array_equal(out[0].cpu().numpy().reshape(-1, 5), ref["rois"].reshape(-1, 5))
+    gp = dict(m.named_parameters())
+    errs = {}
+    for k, p in o.named_parameters():
+        if p.requires_grad:
+            a, b = gp[k].grad.detach().double().cpu(), p.grad.double()
+            errs[k] = float((a - b).norm() / max(b.norm(), 1e-12))
+    bad = {k: e for k, e in errs.items() if not e < 1e-2}
+    assert not bad, bad

@@ -41,6 +41,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+// Fused epilogue: y = act(acc * scale[co] + bias[co] + residual[n,co,p]); every pointer
+// optional.  scale/bias carry a frozen BatchNorm folded per channel (ResNet: BN in eval
+// mode with frozen affine, lib/DAF/resnet.py:261-284); residual is the bottleneck's
+// identity/downsample branch (resnet.py:94-97).
+struct Epi {
+  const float* scale;
+  const float* bias;
+  const float* residual;
+  int relu;
+};
+
 // ======================================================================= forward
 // Block tile: BM = WM*MI*32 output channels x BN = TH*32 pixels (TH = WN*NJ rows of 32).
 // K is consumed in chunks of CK input channels (KC = CK*KS*KS).  The 32x32x2 MFMA pairs
@@ -63,14 +74,14 @@ struct FwdCfg {
   static constexpr int A_V4 = A_ELEMS / 4;
   static constexpr int A_PER = (A_V4 + NT - 1) / NT;
   static constexpr int B_PER = (B_ELEMS + NT - 1) / NT;
-  static constexpr int LDS_FLOATS = 2 * (A_ELEMS + B_ELEMS) + BM;  // + bias tile
+  static constexpr int LDS_FLOATS = 2 * (A_ELEMS + B_ELEMS) + 2 * BM;  // + scale/bias tiles
 };
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
 __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
-    const float* __restrict__ X, const float* __restrict__ Wk, const float* __restrict__ bias,
-    float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int relu, int tiles_m,
-    int tiles_w, int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab) {
+    const float* __restrict__ X, const float* __restrict__ Wk, Epi epi, float* __restrict__ Y,
+    int N, int Cin, int H, int W, int Cout, int tiles_m, int tiles_w, int tiles_h, int dp_tiles,
+    int ksplit, int cps, float* __restrict__ slab) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 
@@ -203,10 +214,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   float* bias_s = lds + 2 * (C::A_ELEMS + C::B_ELEMS);
+  float* scale_s = bias_s + C::BM;
   if (tid < C::BM) {
-    const int co = m0 + tid;
-    const float bv = bias ? bias[co < Cout ? co : 0] : 0.f;
-    bias_s[tid] = (bias && co < Cout) ? bv : 0.f;
+    const int co = min(m0 + tid, Cout - 1);
+    bias_s[tid] = epi.bias ? epi.bias[co] : 0.f;
+    scale_s[tid] = epi.scale ? epi.scale[co] : 1.f;
   }
   const int c_begin = direct ? 0 : split * cps;
   const int c_end = direct ? nchunks : min(nchunks, c_begin + cps);
@@ -261,6 +273,8 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     return;
   }
   float* Yn = Y + (size_t)n * Cout * H * W;
+  const float* Rn = epi.residual ? epi.residual + (size_t)n * Cout * H * W : nullptr;
+  const bool has_scale = epi.scale != nullptr;
   const int w = w0 + l32;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -273,9 +287,13 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
         const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         const int co = m0 + ml;
         if (co < Cout) {
-          float v = acc[i][j][r] + bias_s[ml];
-          if (relu) v = fmaxf(v, 0.f);
-          Yn[((size_t)co * H + h) * W + w] = v;
+          const size_t idx = ((size_t)co * H + h) * W + w;
+          float v = acc[i][j][r];
+          if (has_scale) v *= scale_s[ml];
+          v += bias_s[ml];
+          if (Rn) v += Rn[idx];
+          if (epi.relu) v = fmaxf(v, 0.f);
+          Yn[idx] = v;
         }
       }
     }
@@ -488,11 +506,11 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
 
 // y = act(sum_s slab[s] + bias), summed in split order (deterministic).
 // Sum the split-K partial tiles of the tail tiles in fixed split order (deterministic),
-// add bias, apply ReLU and scatter to Y.  One workgroup per (tail tile, 1024 elements).
+// apply the epilogue and scatter to Y.  One workgroup per (tail tile, 1024 elements).
 __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
     const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int th_rows,
-    int tiles_m, int tiles_w, int tiles_h, const float* __restrict__ bias, int Cout, int H, int W,
-    int relu, float* __restrict__ Y) {
+    int tiles_m, int tiles_w, int tiles_h, Epi epi, int Cout, int H, int W,
+    float* __restrict__ Y) {
   const int tp = th_rows * 32, tile_elems = bm * tp;
   const int per_tile = (tile_elems + 1023) / 1024;
   const int ti = blockIdx.x / per_tile;
@@ -510,9 +528,12 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
     if (co >= Cout || h >= H || w >= W) continue;
     float v = S[e];
     for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
-    if (bias) v += bias[co];
-    if (relu) v = fmaxf(v, 0.f);
-    Y[(((size_t)n * Cout + co) * H + h) * W + w] = v;
+    const size_t idx = (((size_t)n * Cout + co) * H + h) * W + w;
+    if (epi.scale) v *= epi.scale[co];
+    if (epi.bias) v += epi.bias[co];
+    if (epi.residual) v += epi.residual[idx];
+    if (epi.relu) v = fmaxf(v, 0.f);
+    Y[idx] = v;
   }
 }
 
@@ -543,20 +564,26 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ Wt, float* __restric
   }
 }
 
-// G = dY * (Y > 0) (when Y given), db[co] (+)= sum over n,p of G.  grid (Cout, N).
+// G0 = dY * (Y > 0) (when Y given); db[co] (+)= sum over n,p of G0; G = G0 * scale[co]
+// (scale: a folded frozen BatchNorm, optional); G0 also stored to Graw when given (the
+// residual branch of a bottleneck takes the unscaled gradient).  grid (Cout, N).
 __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restrict__ dY,
                                                             const float* __restrict__ Y,
+                                                            const float* __restrict__ scale,
                                                             float* __restrict__ G,
+                                                            float* __restrict__ Graw,
                                                             float* __restrict__ db, int Cout,
                                                             int HW) {
   const int co = blockIdx.x, n = blockIdx.y;
   const size_t base = ((size_t)n * Cout + co) * HW;
+  const float sc = scale ? scale[co] : 1.f;
   float s = 0.f;
   const bool vec = (HW % 4) == 0;
   if (vec) {
     const float4* d4 = reinterpret_cast<const float4*>(dY + base);
     const float4* y4 = Y ? reinterpret_cast<const float4*>(Y + base) : nullptr;
     float4* g4 = reinterpret_cast<float4*>(G + base);
+    float4* r4 = Graw ? reinterpret_cast<float4*>(Graw + base) : nullptr;
     for (int i = threadIdx.x; i < HW / 4; i += 256) {
       float4 d = d4[i];
       if (y4) {
@@ -564,15 +591,18 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
         d.x = y.x > 0.f ? d.x : 0.f; d.y = y.y > 0.f ? d.y : 0.f;
         d.z = y.z > 0.f ? d.z : 0.f; d.w = y.w > 0.f ? d.w : 0.f;
       }
-      if (G != dY || y4) g4[i] = d;
+      if (r4) r4[i] = d;
       s += (d.x + d.y) + (d.z + d.w);
+      if (scale) { d.x *= sc; d.y *= sc; d.z *= sc; d.w *= sc; }
+      if (G != dY || y4 || scale) g4[i] = d;
     }
   } else {
     for (int i = threadIdx.x; i < HW; i += 256) {
       float d = dY[base + i];
       if (Y) d = Y[base + i] > 0.f ? d : 0.f;
-      G[base + i] = d;
+      if (Graw) Graw[base + i] = d;
       s += d;
+      G[base + i] = scale ? d * sc : d;
     }
   }
   if (!db) return;
@@ -666,9 +696,8 @@ static FwdPlan plan_fwd(int N, int Cin, int H, int W, int Cout) {
 }
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
-static int launch_fwd(const float* X, const float* Wk, const float* bias, float* Y, int N,
-                      int Cin, int H, int W, int Cout, int relu, float* slab, size_t slab_bytes,
-                      hipStream_t s) {
+static int launch_fwd(const float* X, const float* Wk, Epi epi, float* Y, int N, int Cin, int H,
+                      int W, int Cout, float* slab, size_t slab_bytes, hipStream_t s) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
   const FwdPlan p = plan_fwd<WM, WN, MI, NJ, CK, KS>(N, Cin, H, W, Cout);
   const long long nwg = (long long)p.dp_tiles + (long long)p.n_tail() * (p.ksplit > 1 ? p.ksplit : 0);
@@ -684,34 +713,32 @@ static int launch_fwd(const float* X, const float* Wk, const float* bias, float*
     TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wk, bias, Y, N, Cin, H, W,
-                     Cout, relu, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps,
-                     slab);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wk, epi, Y, N, Cin, H, W,
+                     Cout, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps, slab);
   TLOD_LAUNCH_CHECK();
   if (p.ksplit > 1) {
     const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
     hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
                        p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
-                       p.tiles_h, bias, Cout, H, W, relu, Y);
+                       p.tiles_h, epi, Cout, H, W, Y);
     TLOD_LAUNCH_CHECK();
   }
   return kOk;
 }
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS>
-static int launch_fwd_v(const float* X, const float* Wk, const float* bias, float* Y, int N,
-                        int Cin, int H, int W, int Cout, int relu, float* slab, size_t sb,
-                        hipStream_t s) {
+static int launch_fwd_v(const float* X, const float* Wk, Epi epi, float* Y, int N, int Cin,
+                        int H, int W, int Cout, float* slab, size_t sb, hipStream_t s) {
   if ((Cout & 3) == 0)
-    return launch_fwd<WM, WN, MI, NJ, CK, KS, true>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, slab, sb, s);
-  return launch_fwd<WM, WN, MI, NJ, CK, KS, false>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, slab, sb, s);
+    return launch_fwd<WM, WN, MI, NJ, CK, KS, true>(X, Wk, epi, Y, N, Cin, H, W, Cout, slab, sb, s);
+  return launch_fwd<WM, WN, MI, NJ, CK, KS, false>(X, Wk, epi, Y, N, Cin, H, W, Cout, slab, sb, s);
 }
 
 // Dispatch on (KS, Cout): the tile configs used by the backbone.  ws_query != nullptr:
 // only report the split-K slab bytes the call would need.
-static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias, float* Y, int N,
-                             int Cin, int H, int W, int Cout, int KS, int relu, float* slab,
-                             size_t sb, hipStream_t s, size_t* ws_query = nullptr) {
+static int conv_fwd_dispatch(const float* X, const float* Wk, Epi epi, float* Y, int N,
+                             int Cin, int H, int W, int Cout, int KS, float* slab, size_t sb,
+                             hipStream_t s, size_t* ws_query = nullptr) {
 #define TLOD_FWD_CFG(WM_, WN_, MI_, NJ_, CK_, KS_)                                              \
   do {                                                                                          \
     if (ws_query) {                                                                             \
@@ -720,8 +747,8 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, const float* bias,
                       .slab_bytes(C_::BM, C_::TH);                                              \
       return kOk;                                                                               \
     }                                                                                           \
-    return launch_fwd_v<WM_, WN_, MI_, NJ_, CK_, KS_>(X, Wk, bias, Y, N, Cin, H, W, Cout, relu, \
-                                                       slab, sb, s);                            \
+    return launch_fwd_v<WM_, WN_, MI_, NJ_, CK_, KS_>(X, Wk, epi, Y, N, Cin, H, W, Cout, slab,  \
+                                                       sb, s);                                  \
   } while (0)
   if (KS == 3) {
     if (Cout <= 64) TLOD_FWD_CFG(1, 8, 2, 2, 8, 3);
@@ -825,8 +852,8 @@ extern "C" int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, 
 
 extern "C" size_t tlod_conv_fwd_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS) {
   size_t b = 0;
-  conv_fwd_dispatch(nullptr, nullptr, nullptr, nullptr, N, Cin, H, W, Cout, KS, 0, nullptr, 0,
-                    nullptr, &b);
+  conv_fwd_dispatch(nullptr, nullptr, Epi{}, nullptr, N, Cin, H, W, Cout, KS, nullptr, 0, nullptr,
+                    &b);
   return b;
 }
 
@@ -838,8 +865,18 @@ extern "C" int tlod_conv_fwd_f32(const float* x, const float* wk, const float* b
                                  int N, int Cin, int H, int W, int Cout, int KS, int relu,
                                  void* ws, size_t ws_bytes, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
-  return conv_fwd_dispatch(x, wk, bias, y, N, Cin, H, W, Cout, KS, relu, (float*)ws, ws_bytes,
-                           (hipStream_t)stream);
+  return conv_fwd_dispatch(x, wk, Epi{nullptr, bias, nullptr, relu}, y, N, Cin, H, W, Cout, KS,
+                           (float*)ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int tlod_conv_fwd_ex_f32(const float* x, const float* wk, const float* scale,
+                                    const float* bias, const float* residual, float* y, int N,
+                                    int Cin, int H, int W, int Cout, int KS, int relu, void* ws,
+                                    size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
+  TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
+  return conv_fwd_dispatch(x, wk, Epi{scale, bias, residual, relu}, y, N, Cin, H, W, Cout, KS,
+                           (float*)ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, int N, int Cin,
@@ -847,7 +884,7 @@ extern "C" int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, 
                                    tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
   // dx[n, ci] = sum_{co, s'} Wd[(co, s')][ci] * dy[n, co, p + s' - pad]: forward form
-  return conv_fwd_dispatch(dy, wd, nullptr, dx, N, Cout, H, W, Cin, KS, 0, (float*)ws, ws_bytes,
+  return conv_fwd_dispatch(dy, wd, Epi{}, dx, N, Cout, H, W, Cin, KS, (float*)ws, ws_bytes,
                            (hipStream_t)stream);
 }
 
@@ -883,8 +920,19 @@ extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, i
 extern "C" int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db,
                                       int N, int C, int HW, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0, "bad shape");
-  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C, N), dim3(256), 0, (hipStream_t)stream, dy, y, g,
-                     db, C, HW);
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C, N), dim3(256), 0, (hipStream_t)stream, dy, y,
+                     nullptr, g, nullptr, db, C, HW);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float* scale, float* g,
+                                    float* g_raw, float* db, int N, int C, int HW,
+                                    tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0 && dy && g, "bad arguments");
+  TLOD_CHECK_ARG(g_raw != g || g_raw == nullptr, "g_raw must not alias g");
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C, N), dim3(256), 0, (hipStream_t)stream, dy, y,
+                     scale, g, g_raw, db, C, HW);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

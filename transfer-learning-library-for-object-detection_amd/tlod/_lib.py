@@ -83,6 +83,12 @@ SIGNATURES = {
                                     c_size_t, P]),
     "tlod_relu_bwd_bias_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, P]),
     "tlod_sgd_clip_f32": (c_int, [P, c_int, c_float, c_float, P, P, P]),
+    "tlod_conv_fwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_int, P, c_size_t, P]),
+    "tlod_relu_bwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, P]),
+    "tlod_stem_conv7x7s2_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_space_to_depth_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_depth_to_space_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
 }

@@ -61,7 +61,8 @@ def pack_dgrad(weight):
     return wd
 
 
-def conv_fwd(x, weight, bias=None, relu=False, wk=None):
+def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=None):
+    """y = act(conv(x, weight) * scale + bias + residual) (tlod_conv_fwd_ex_f32)."""
     _check(x, weight)
     x = x.contiguous()
     N, Cin, H, W = x.shape
@@ -69,11 +70,16 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None):
     wk = pack_fwd(weight) if wk is None else wk
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
+    sc = scale.detach().contiguous() if scale is not None else None
+    res = residual.detach().contiguous() if residual is not None else None
+    if res is not None:
+        assert res.shape == y.shape, (res.shape, y.shape)
     L = _lib.lib()
     ws = _lib.workspace(L.tlod_conv_fwd_workspace_bytes(N, Cin, H, W, Cout, KS), x.device, "conv")
     _timed("fwd", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
-        L.tlod_conv_fwd_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(b), _lib.ptr(y), N, Cin, H, W, Cout,
-                            KS, int(relu), _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv_fwd"))
+        L.tlod_conv_fwd_ex_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(sc), _lib.ptr(b),
+                               _lib.ptr(res), _lib.ptr(y), N, Cin, H, W, Cout, KS, int(relu),
+                               _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv_fwd"))
     return y
 
 
@@ -136,6 +142,42 @@ class ConvFunction(torch.autograd.Function):
         dx = conv_dgrad(g, weight) if need_x else None
         dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
         return dx, dw, db, None
+
+
+def relu_bwd_ex(dy, y=None, scale=None, want_raw=False):
+    """g0 = dy * (y > 0) (y None: dy); returns (g0 * scale, g0 or None)."""
+    dy = dy.contiguous()
+    N, C, H, W = dy.shape
+    g = torch.empty_like(dy)
+    raw = torch.empty_like(dy) if want_raw else None
+    _lib.check(_lib.lib().tlod_relu_bwd_ex_f32(
+        _lib.ptr(dy), _lib.ptr(y.contiguous() if y is not None else None),
+        _lib.ptr(scale.detach().contiguous() if scale is not None else None), _lib.ptr(g),
+        _lib.ptr(raw), None, N, C, H * W, _lib.stream_of(dy)), "relu_bwd_ex")
+    return g, raw
+
+
+class ConvBNFunction(torch.autograd.Function):
+    """Bias-free conv + frozen BatchNorm (per-channel scale/shift) (+ residual) (+ ReLU), the
+    ResNet bottleneck's conv->bn(->add)->relu (lib/DAF/resnet.py:80-99) in one kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, scale, shift, residual, relu):
+        y = conv_fwd(x, weight, shift, relu, scale=scale, residual=residual)
+        ctx.relu = bool(relu)
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, weight, scale, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, scale, y = ctx.saved_tensors
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_res = ctx.has_res and ctx.needs_input_grad[4]
+        g, g_raw = relu_bwd_ex(dy, y if ctx.relu else None, scale, want_raw=need_res)
+        dx = conv_dgrad(g, weight) if need_x else None
+        dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
+        return dx, dw, None, None, g_raw, None
 
 
 class Conv2d(nn.Conv2d):

@@ -269,3 +269,38 @@ class vgg16(_fasterRCNN):
 
     def _head_to_tail(self, pool5):
         return self.RCNN_top(pool5.view(pool5.size(0), -1))
+
+
+class resnet(_fasterRCNN):
+    """lib/DAF/resnet.py:220-288 (ResNet101; random init — the caffe weights are external).
+
+    Deviation, documented: the reference's _InstanceDA is Linear(4096, ...) (DA.py:56)
+    and crashes on the 2048-d ResNet head features; here the instance head takes 2048."""
+
+    def __init__(self, classes, num_layers=101, pretrained=False, class_agnostic=False):
+        if num_layers != 101:
+            raise NotImplementedError("only ResNet101 (the reference's only depth)")
+        self.dout_base_model = 1024
+        self.instance_dim = 2048
+        self.pretrained = pretrained
+        self.class_agnostic = class_agnostic
+        _fasterRCNN.__init__(self, classes, class_agnostic)
+
+    def _init_modules(self):
+        from ..detector.resnet import resnet101_parts
+        self.RCNN_base, self.RCNN_top = resnet101_parts(cfg.RESNET.FIXED_BLOCKS)
+        self.RCNN_cls_score = nn.Linear(2048, self.n_classes)
+        self.RCNN_bbox_pred = nn.Linear(2048, 4 if self.class_agnostic else 4 * self.n_classes)
+
+    def train(self, mode=True):
+        """resnet.py:269-284: BatchNorm stays in eval mode."""
+        nn.Module.train(self, mode)
+        if mode:
+            from ..detector.resnet import set_bn_eval
+            set_bn_eval(self.RCNN_base)
+            set_bn_eval(self.RCNN_top)
+        return self
+
+    def _head_to_tail(self, pool5):
+        # RCNN_top(pool5).mean(3).mean(2) (resnet.py:286-288); the head runs channels-last
+        return self.RCNN_top(pool5).mean(2).mean(1)

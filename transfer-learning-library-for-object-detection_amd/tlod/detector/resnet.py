@@ -1,0 +1,206 @@
+"""ResNet101 backbone and head for the DAF/MAF/ATF detectors (lib/DAF/resnet.py:57-288).
+
+Same modules and state_dict keys as the reference (``RCNN_base`` = Sequential(conv1, bn1,
+relu, maxpool, layer1, layer2, layer3), ``RCNN_top`` = Sequential(layer4); Bottleneck
+conv1/bn1/conv2/bn2/conv3/bn3/downsample), the caffe-style stride on the bottleneck's 1x1
+conv1 (:71), maxpool ceil_mode (:113), frozen conv1/bn1/layer1 and every BatchNorm frozen
+in eval mode (:249-284).  Execution:
+
+  * every BatchNorm is frozen and in eval mode, i.e. a per-channel affine, folded into
+    the producing conv's epilogue (tlod_conv_fwd_ex_f32: conv * scale + shift
+    (+ residual) (+ ReLU)) — one kernel per conv, no separate BN / add / ReLU passes;
+  * stride-2 1x1 convs run as the stride-1 conv of x[:, :, ::2, ::2] (tlod_subsample2_f32;
+    conv1 and the downsample share the subsampled tensor);
+  * the stem (7x7/2 conv + bn1 + ReLU, frozen) is tlod_stem_conv7x7s2_f32;
+  * the RoI head (layer4 on R x 1024 x 7x7 -> 4x4 maps) runs channels-last: 1x1 convs
+    are plain GEMMs and the 3x3 convs GEMMs over a 9-tap gather (hipBLASLt through
+    torch.matmul) — 4x4 maps would fill 16 of the 256 pixel slots of a conv tile.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib
+from ..conv import ConvBNFunction
+
+
+def fold_bn(bn):
+    """Frozen eval-mode BatchNorm as y = x * scale + shift (per channel)."""
+    assert not bn.weight.requires_grad, "tlod ResNet expects frozen BatchNorm (resnet.py:261-267)"
+    with torch.no_grad():
+        scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        shift = bn.bias - bn.running_mean * scale
+    return scale.contiguous(), shift.contiguous()
+
+
+class Subsample2Function(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _lib.require_cuda(x)
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty((N, C, (H + 1) // 2, (W + 1) // 2), dtype=x.dtype, device=x.device)
+        _lib.check(_lib.lib().tlod_subsample2_f32(_lib.ptr(x), N, C, H, W, _lib.ptr(y),
+                                                  _lib.stream_of(x)), "subsample2")
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        g = g.contiguous()
+        dx = torch.empty((N, C, H, W), dtype=g.dtype, device=g.device)
+        _lib.check(_lib.lib().tlod_upsample2_zero_f32(_lib.ptr(g), N, C, H, W, _lib.ptr(dx),
+                                                      _lib.stream_of(g)), "upsample2_zero")
+        return dx
+
+
+def conv_bn(x, conv, bn, relu, residual=None):
+    scale, shift = fold_bn(bn)
+    return ConvBNFunction.apply(x, conv.weight, scale, shift, residual, relu)
+
+
+def stem(x, conv1, bn1):
+    """conv1 7x7/2 + bn1 + ReLU (resnet.py:107-110; frozen: forward only)."""
+    _lib.require_cuda(x)
+    assert not conv1.weight.requires_grad
+    x = x.contiguous()
+    N, _, H, W = x.shape
+    scale, shift = fold_bn(bn1)
+    y = torch.empty((N, 64, (H - 1) // 2 + 1, (W - 1) // 2 + 1), dtype=x.dtype, device=x.device)
+    _lib.check(_lib.lib().tlod_stem_conv7x7s2_f32(
+        _lib.ptr(x), _lib.ptr(conv1.weight.detach().contiguous()), _lib.ptr(scale),
+        _lib.ptr(shift), _lib.ptr(y), N, H, W, 1, _lib.stream_of(x)), "stem_conv")
+    return y
+
+
+class Bottleneck(nn.Module):
+    """resnet.py:64-102 (modules for parameters/keys; forward on the fused kernels)."""
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, kernel_size=1, stride=stride, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, stride=1, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, kernel_size=1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        xs = Subsample2Function.apply(x) if self.stride == 2 else x
+        out = conv_bn(xs, self.conv1, self.bn1, relu=True)
+        out = conv_bn(out, self.conv2, self.bn2, relu=True)
+        res = (conv_bn(xs, self.downsample[0], self.downsample[1], relu=False)
+               if self.downsample is not None else x)
+        return conv_bn(out, self.conv3, self.bn3, relu=True, residual=res)
+
+    # ---------------------------------------------------------------- RoI head path
+    @staticmethod
+    def _gemm_bn(xm, conv, bn, relu, residual=None):
+        """xm: (P, Cin) channels-last rows; conv as a GEMM + folded BN (+res) (+ReLU)."""
+        scale, shift = fold_bn(bn)
+        w = conv.weight
+        if w.shape[2] == 1:
+            y = xm @ w.view(w.shape[0], -1).t()
+        else:
+            y = xm @ w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).t()
+        y = y * scale + shift
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
+
+    def forward_nhwc(self, x):
+        """x: (R, H, W, C) channels-last (the layer4 RoI head)."""
+        if self.stride == 2:
+            x = x[:, ::2, ::2, :]
+        R, H, W, C = x.shape
+        xm = x.reshape(R * H * W, C)
+        out = self._gemm_bn(xm, self.conv1, self.bn1, relu=True)
+        P = out.shape[1]
+        pad = F.pad(out.view(R, H, W, P), (0, 0, 1, 1, 1, 1))
+        taps = torch.cat([pad[:, kh:kh + H, kw:kw + W, :] for kh in range(3) for kw in range(3)], 3)
+        out = self._gemm_bn(taps.reshape(R * H * W, 9 * P), self.conv2, self.bn2, relu=True)
+        res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False)
+               if self.downsample is not None else xm)
+        out = self._gemm_bn(out, self.conv3, self.bn3, relu=True, residual=res)
+        return out.view(R, H, W, -1)
+
+
+class ResNetBase(nn.Sequential):
+    """RCNN_base = Sequential(conv1, bn1, relu, maxpool, layer1, layer2, layer3)."""
+
+    def forward(self, x):
+        conv1, bn1, _, maxpool, *layers = list(self)
+        x = stem(x, conv1, bn1)
+        x = F.max_pool2d(x, maxpool.kernel_size, maxpool.stride, maxpool.padding,
+                         ceil_mode=maxpool.ceil_mode)
+        for layer in layers:
+            x = layer(x)
+        return x
+
+
+class ResNetTop(nn.Sequential):
+    """RCNN_top = Sequential(layer4); forward(pool5 NCHW) -> channels-last features."""
+
+    def forward(self, pool5):
+        x = pool5.permute(0, 2, 3, 1)
+        for block in self[0]:
+            x = block.forward_nhwc(x)
+        return x
+
+
+def _make_layer(inplanes, planes, blocks, stride=1):
+    downsample = None
+    if stride != 1 or inplanes != planes * 4:
+        downsample = nn.Sequential(
+            nn.Conv2d(inplanes, planes * 4, kernel_size=1, stride=stride, bias=False),
+            nn.BatchNorm2d(planes * 4))
+    layers = [Bottleneck(inplanes, planes, stride, downsample)]
+    for _ in range(1, blocks):
+        layers.append(Bottleneck(planes * 4, planes))
+    return nn.Sequential(*layers)
+
+
+def resnet101_parts(fixed_blocks=1):
+    """(RCNN_base, RCNN_top) of resnet101() with the reference init (resnet.py:120-128:
+    conv N(0, sqrt(2/(k*k*out))), BN weight 1 / bias 0) and freezing (:249-267)."""
+    conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+    bn1 = nn.BatchNorm2d(64)
+    maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=0, ceil_mode=True)
+    layer1 = _make_layer(64, 64, 3)
+    layer2 = _make_layer(256, 128, 4, stride=2)
+    layer3 = _make_layer(512, 256, 23, stride=2)
+    layer4 = _make_layer(1024, 512, 3, stride=2)
+    base = ResNetBase(conv1, bn1, nn.ReLU(inplace=True), maxpool, layer1, layer2, layer3)
+    top = ResNetTop(layer4)
+    for m in list(base.modules()) + list(top.modules()):
+        if isinstance(m, nn.Conv2d):
+            n = m.kernel_size[0] * m.kernel_size[1] * m.out_channels
+            m.weight.data.normal_(0, math.sqrt(2.0 / n))
+        elif isinstance(m, nn.BatchNorm2d):
+            m.weight.data.fill_(1)
+            m.bias.data.zero_()
+    for p in list(base[0].parameters()) + list(base[1].parameters()):
+        p.requires_grad = False
+    assert 0 <= fixed_blocks < 4
+    for idx in range(4, 4 + fixed_blocks):  # layer1 (.. layer3)
+        for p in base[idx].parameters():
+            p.requires_grad = False
+    for m in list(base.modules()) + list(top.modules()):
+        if isinstance(m, nn.BatchNorm2d):
+            for p in m.parameters():
+                p.requires_grad = False
+    return base, top
+
+
+def set_bn_eval(module):
+    """resnet.py:269-284: BatchNorm always in eval mode (frozen running statistics)."""
+    for m in module.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m.eval()

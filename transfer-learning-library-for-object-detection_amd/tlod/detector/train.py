@@ -21,22 +21,24 @@ METHODS = ("daf", "maf", "atf")
 
 
 def build_model(method, device, net="vgg16", classes=CITYSCAPES_CLASSES, seed=0):
-    """<method>.vgg16(classes).create_architecture() (methods/<M>/<M>_train.py), random
+    """<method>.<net>(classes).create_architecture() (methods/<M>/<M>_train.py), random
     init (the pretrained caffe weights are external downloads)."""
-    if method == "daf":
-        from ..da.daf import vgg16
-    elif method == "maf":
-        from ..da.maf import vgg16
-    elif method == "atf":
-        from ..da.atf import vgg16
-    else:
+    if method not in METHODS:
         raise ValueError(f"unknown method {method!r} (have {METHODS})")
-    if net != "vgg16":
-        raise NotImplementedError(f"backbone {net!r}")
+    if net not in ("vgg16", "res101"):
+        raise ValueError(f"unknown backbone {net!r}")
+    import importlib
+    mod = importlib.import_module(f"..da.{method}", __package__)
+    if net == "res101" and not hasattr(mod, "resnet"):
+        raise NotImplementedError(f"{method} with ResNet101")
     setup_training_cfg(net)
     torch.manual_seed(seed)
-    m = vgg16(classes, pretrained=False, class_agnostic=False)
+    if net == "vgg16":
+        m = mod.vgg16(classes, pretrained=False, class_agnostic=False)
+    else:
+        m = mod.resnet(classes, 101, pretrained=False, class_agnostic=False)
     m.create_architecture()
+    m.net = net
     return m.to(device).train()
 
 
@@ -45,9 +47,12 @@ def build_daf_vgg16(device, classes=CITYSCAPES_CLASSES, seed=0):
 
 
 def make_optimizer(model, lr, momentum=None, weight_decay=None, double_bias=None, bias_decay=None,
-                   fused=True, clip=10.0):
+                   fused=True, clip=None):
     """DAF_train.py:311-325 param groups (collapsed to two groups — same update).
-    fused=True: libtlod's fused clip_gradient(clip) + SGD (tlod.optim.FusedSGDClip)."""
+    fused=True: libtlod's fused clip_gradient(clip) + SGD (tlod.optim.FusedSGDClip).
+    clip None: 10 for VGG16, none for ResNet101 (DAF_train.py:406-407)."""
+    if clip is None:
+        clip = default_clip(model)
     momentum = cfg.TRAIN.MOMENTUM if momentum is None else momentum
     wd = cfg.TRAIN.WEIGHT_DECAY if weight_decay is None else weight_decay
     double_bias = cfg.TRAIN.DOUBLE_BIAS if double_bias is None else double_bias
@@ -125,7 +130,11 @@ def daf_loss(out, lamda=0.1):
     return _fasterRCNN.total_loss(out, lamda)
 
 
-def train_step(model, optimizer, batch, lamda=0.1, clip=10.0, reducer=None):
+def default_clip(model):
+    return 10.0 if getattr(model, "net", "vgg16") == "vgg16" else 0.0
+
+
+def train_step(model, optimizer, batch, lamda=0.1, clip=None, reducer=None):
     """One DAF/MAF/ATF iteration (the method's own loss sum, model.total_loss); returns the
     loss as a device tensor (no host sync)."""
     if reducer is not None:
@@ -141,15 +150,16 @@ def train_step(model, optimizer, batch, lamda=0.1, clip=10.0, reducer=None):
     if isinstance(optimizer, FusedSGDClip):
         optimizer.step()  # clip_gradient + SGD fused
     else:
+        clip = default_clip(model) if clip is None else clip
         if clip:
             clip_gradient_([p for p in model.parameters()], clip)
         optimizer.step()
     return loss.detach()
 
 
-def smoke_step(device, method="daf"):
-    """One tiny <method>-VGG16 forward+backward+update on `device` (used by smoke())."""
-    model = build_model(method, device)
+def smoke_step(device, method="daf", net="vgg16"):
+    """One tiny <method>-<net> forward+backward+update on `device` (used by smoke())."""
+    model = build_model(method, device, net)
     opt = make_optimizer(model, 2e-3)
     data = SyntheticCityscapes(device, H=192, W=320, G=4, pool=1, seed=7)
     loss = train_step(model, opt, data.next())
