@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--cpu-baseline-steps", type=int, default=2,
                     help="oracle CPU steps timed on rank 0 at N=1 (0 disables)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--net", choices=("vgg16", "res101"), default="vgg16")
     ap.add_argument("--method", choices=("daf", "maf", "atf"), default="daf",
                     help="detector (the headline metric is DAF; MAF / ATF are secondary workloads)")
     return ap.parse_args()
@@ -93,8 +94,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    model = build_model(a.method, dev)
-    opt = make_optimizer(model, 2e-3)
+    model = build_model(a.method, dev, a.net)
+    # clip_gradient(10) also for ResNet101 (the reference clips VGG16 only, DAF_train.py:406):
+    # with random-init weights the unclipped first steps diverge; the fused step does the
+    # same work either way (the norm is always computed)
+    opt = make_optimizer(model, 2e-3, clip=10.0)
     reducer = GradBucketReducer(model, bucket_mb=a.bucket_mb) if world > 1 else None
     data = SyntheticCityscapes(dev, H=a.height, W=a.width, seed=1000 * rank + 1)
 
@@ -126,18 +130,19 @@ def main():
 
     achieved, detail, conv_ms, conv_f, n_launch = conv_roofline(records)
     result = {
-        "metric": METRIC if a.method == "daf" else METRIC.replace("DAF", a.method.upper()),
+        "metric": METRIC.replace("DAF VGG16", f"{a.method.upper()} {'VGG16' if a.net == 'vgg16' else 'ResNet101'}"),
         "value": round(value, 4), "unit": "img/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"{a.method.upper()} VGG16 Cityscapes->Foggy training step "
+        "config": {"workload": f"{a.method.upper()} {a.net} Cityscapes->Foggy training step "
                                f"(methods/{a.method.upper()}/{a.method.upper()}_train.py), "
                                "1 source + 1 target image per GPU per step",
                    "image_hw": [a.height, a.width], "source_images_per_step": world,
                    "images_processed_per_step": 2 * world, "parallelism": f"dp{world}",
                    "classes": 9, "rpn_pre_post_nms_train": [12000, 2000],
-                   "rpn_pre_post_nms_test": [6000, 300], "rcnn_batch": 256},
+                   "rpn_pre_post_nms_test": [6000, 300],
+                   "rcnn_batch": 256 if a.net == "vgg16" else 128},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                      "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
@@ -147,7 +152,8 @@ def main():
         "mean_loss": round(last_loss, 4),
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and a.cpu_baseline_steps > 0 and a.method == "daf":
+    if rank == 0 and world == 1 and a.cpu_baseline_steps > 0 and a.method == "daf" \
+            and a.net == "vgg16":
         result["cpu_baseline"] = cpu_baseline(a.cpu_baseline_steps, a.height, a.width)
     if rank == 0:
         print(json.dumps(result), flush=True)

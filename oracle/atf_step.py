@@ -17,10 +17,11 @@ from .daf_step import CFG, OracleDAF, _RoIAlignAvgCPU, _smooth_l1
 
 
 class OracleATF(OracleDAF):
-    def __init__(self, n_classes=9, dropout=0.5):
-        super().__init__(n_classes, dropout)
+    def __init__(self, n_classes=9, dropout=0.5, backbone="vgg16"):
+        super().__init__(n_classes, dropout, backbone)
+        shared = self.splits[0]
         layers = list(self.RCNN_base)
-        self.RCNN_base_t = nn.Sequential(*(layers[:10] + [copy.deepcopy(m) for m in layers[10:]]))
+        self.RCNN_base_t = nn.Sequential(*(layers[:shared] + [copy.deepcopy(m) for m in layers[shared:]]))
         for name, dim in (("RCNN_imageDA_3", 256), ("RCNN_imageDA_4", 512)):
             m = nn.Module()
             m.Conv1 = nn.Conv2d(dim, 512, 1, bias=False)
@@ -66,15 +67,16 @@ class OracleATF(OracleDAF):
         (im, info, gt, num, need, t_im, t_info, t_gt, t_num, t_need) = batch
         c = CFG
         ov = rois_override or (None, None, None)
+        _, e3, e4 = self.splits
         base = self.RCNN_base(im)
-        c3_t = self.RCNN_base_t[:16](im)
-        c4_t = self.RCNN_base_t[16:23](c3_t)
-        base_t = self.RCNN_base_t[23:](c4_t)
+        c3_t = self.RCNN_base_t[:e3](im)
+        c4_t = self.RCNN_base_t[e3:e4](c3_t)
+        base_t = self.RCNN_base_t[e4:](c4_t)
         rois_domain, l1c, l1b = self._rpn_train(base, gt, info, rng, ov[0])
         rois_domain_t, l2c, l2b = self._rpn_train(base_t, gt, info, rng, ov[1])
 
         def sample(r):
-            r, rl, rt, riw, row = orpn.proposal_target(r, gt.numpy(), rng)
+            r, rl, rt, riw, row = orpn.proposal_target(r, gt.numpy(), rng, self.rcnn_cfg)
             return (r, torch.from_numpy(rl).view(-1).long(), torch.from_numpy(rt).view(-1, 4),
                     torch.from_numpy(riw).view(-1, 4), torch.from_numpy(row).view(-1, 4))
         r_s, rl_s, rt_s, riw_s, row_s = sample(rois_domain)
@@ -82,14 +84,12 @@ class OracleATF(OracleDAF):
 
         def head(feat, rois):
             p = _RoIAlignAvgCPU.apply(feat, torch.from_numpy(rois).view(-1, 5))
-            return self.RCNN_top(p.view(p.size(0), -1))
+            return self._head_to_tail(p)
         fc7_s, fc7_t, fc7_dt = head(base, r_s), head(base_t, r_t), head(base_t, rois_domain_t)
         cls_s, box_s = self._det_losses(fc7_s, rl_s, rt_s, riw_s, row_s)
         cls_t, box_t = self._det_losses(fc7_t, rl_t, rt_t, riw_t, row_t)
 
-        t_c3 = self.RCNN_base[:16](t_im)
-        t_c4 = self.RCNN_base[16:23](t_c3)
-        t_base = self.RCNN_base[23:](t_c4)
+        t_c3, t_c4, t_base = self._backbone(t_im)
         _, _, t_prob, t_bbox = self._rpn(t_base)
         t_rois = orpn.proposal_layer(t_prob.detach().numpy(), t_bbox.detach().numpy(),
                                      t_info.numpy(), self.base_anchors, c["stride"], c["pre_test"],

@@ -81,11 +81,13 @@ class OracleDAF(nn.Module):
             self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), nn.ReLU(True), nn.Dropout(dropout),
                                           nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout))
             din, dfeat = 512, 4096
+            self.splits = (10, 16, 23)  # shared frozen prefix, conv3 end, conv4 end
         else:
             from .resnet import resnet101_parts
             self.RCNN_base, self.RCNN_top = resnet101_parts()
             self.rcnn_cfg["batch"] = 128
             din, dfeat = 1024, 2048
+            self.splits = (5, 5, 6)  # conv1..layer1 | layer2 | layer3
         self.RCNN_cls_score = nn.Linear(dfeat, n_classes)
         self.RCNN_bbox_pred = nn.Linear(dfeat, 4 * n_classes)
         rpn = nn.Module()
@@ -135,13 +137,13 @@ class OracleDAF(nn.Module):
         return self.RCNN_top(pooled.view(pooled.size(0), -1))
 
     def _backbone(self, im):
-        """RCNN_base in the three pieces MAF taps (lib/MAF/vgg16.py:84-86): conv3 =
-        features[:16], conv34 = [16:23], conv45 = [23:-1]."""
-        if self.backbone == "res101":
-            return None, None, self.RCNN_base(im)
-        c3 = self.RCNN_base[:16](im)
-        c4 = self.RCNN_base[16:23](c3)
-        return c3, c4, self.RCNN_base[23:](c4)
+        """RCNN_base in the three pieces MAF / ATF tap (lib/MAF/vgg16.py:84-86): conv3 =
+        features[:16], conv34 = [16:23], conv45 = [23:-1]; ResNet101: conv1..layer1 |
+        layer2 | layer3 (lib/ATF/resnet.py:238-241)."""
+        _, e3, e4 = self.splits
+        c3 = self.RCNN_base[:e3](im)
+        c4 = self.RCNN_base[e3:e4](c3)
+        return c3, c4, self.RCNN_base[e4:](c4)
 
     def _detect(self, batch, rng, rois_override=None):
         """Everything but the DA heads (lib/DAF/faster_rcnn.py:45-175).  rois_override:

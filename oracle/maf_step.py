@@ -46,8 +46,9 @@ class _WGRL(torch.autograd.Function):
 
 
 class OracleMAF(OracleDAF):
-    def __init__(self, n_classes=9, dropout=0.5):
-        super().__init__(n_classes, dropout)
+    def __init__(self, n_classes=9, dropout=0.5, backbone="vgg16"):
+        super().__init__(n_classes, dropout, backbone)
+        dfeat = self.RCNN_cls_score.in_features
         del self.RCNN_instanceDA
         for name, dim, inner, scale in (("RCNN_imageDA_3", 256, 64, 4), ("RCNN_imageDA_4", 512, 256, 2)):
             m = nn.Module()
@@ -58,7 +59,7 @@ class OracleMAF(OracleDAF):
             m.scale = scale
             setattr(self, name, m)
         ins = nn.Module()
-        ins.dc_ip1 = nn.Linear(4096 + n_classes, 1024)
+        ins.dc_ip1 = nn.Linear(dfeat + n_classes, 1024)
         ins.dc_ip2 = nn.Linear(1024, 1024)
         ins.clssifer = nn.Linear(1024, 2)
         self.RCNN_instanceDA = ins

@@ -17,20 +17,22 @@ IDX = [3, 4, 5, 6, 8, 9, 10, 11]
 VIEWS = ("conv3_s.", "conv3_t.", "conv34_s.", "conv34_t.", "conv45_s.", "conv45_t.", "RCNN_rpn_t.")
 
 
-@pytest.mark.parametrize("H,W,seed", [(192, 320, 0), (224, 288, 3)])
-def test_atf_losses_and_grads_match_oracle(H, W, seed):
+@pytest.mark.parametrize("net,H,W,seed", [("vgg16", 192, 320, 0), ("vgg16", 224, 288, 3),
+                                          ("res101", 224, 320, 5)])
+def test_atf_losses_and_grads_match_oracle(net, H, W, seed):
     from oracle.atf_step import OracleATF, total_loss
     from oracle.daf_step import synthetic_batch
     from tlod.config import cfg
     from tlod.detector.train import build_model
-    m = build_model("atf", dev, seed=seed)
+    m = build_model("atf", dev, net=net, seed=seed)
     with torch.no_grad():  # make the two branches differ
-        for p in m.RCNN_base_t[10:].parameters():
-            p.mul_(1.0 + 0.05 * torch.randn_like(p))
+        for p in m.RCNN_base_t[m.splits[0]:].parameters():
+            if p.requires_grad:
+                p.mul_(1.0 + 0.05 * torch.randn_like(p))
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
-    o = OracleATF(dropout=0.0).train()
+    o = OracleATF(dropout=0.0, backbone=net).train()
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items() if not k.startswith(VIEWS)}
     o.load_state_dict(sd, strict=True)
     assert cfg.TEST.RPN_POST_NMS_TOP_N == 300

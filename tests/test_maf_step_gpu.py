@@ -45,16 +45,17 @@ LOSSES = ["rpn_loss_cls", "rpn_loss_box", "RCNN_loss_cls", "RCNN_loss_bbox", "DA
 IDX = [3, 4, 5, 6, 8, 9, 10, 11]
 
 
-@pytest.mark.parametrize("H,W,seed", [(192, 320, 0), (224, 352, 2)])
-def test_maf_losses_and_grads_match_oracle(H, W, seed):
+@pytest.mark.parametrize("net,H,W,seed", [("vgg16", 192, 320, 0), ("vgg16", 224, 352, 2),
+                                          ("res101", 224, 320, 4)])
+def test_maf_losses_and_grads_match_oracle(net, H, W, seed):
     from oracle.daf_step import synthetic_batch
     from oracle.maf_step import OracleMAF, total_loss
     from tlod.detector.train import build_model
-    m = build_model("maf", dev, seed=seed)
+    m = build_model("maf", dev, net=net, seed=seed)
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
-    o = OracleMAF(dropout=0.0).train()
+    o = OracleMAF(dropout=0.0, backbone=net).train()
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()
           if not k.startswith(("conv3.", "conv34.", "conv45."))}  # views of RCNN_base
     o.load_state_dict(sd, strict=True)

@@ -1,0 +1,55 @@
+"""Full-size DAF-ResNet101 forward with finiteness checks at every stage (diagnostics)."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "transfer-learning-library-for-object-detection_amd"))
+import torch
+import torch.nn.functional as F
+from tlod.detector.train import SyntheticCityscapes, build_model
+
+dev = torch.device("cuda")
+m = build_model("daf", dev, "res101")
+data = SyntheticCityscapes(dev, H=600, W=1200, pool=1)
+b = data.next()
+
+
+def chk(name, t):
+    t = t.detach()
+    fin = bool(torch.isfinite(t).all())
+    print(f"{name:28s} {tuple(t.shape)} finite={fin} absmax={float(t.abs().nan_to_num(0, 0, 0).max()):.4g}",
+          flush=True)
+    return fin
+
+
+x = torch.cat([b[0], b[5]], 0)
+for i, mod in enumerate(m.RCNN_base):
+    if i in (1, 2):
+        continue
+    if i == 0:
+        from tlod.detector.resnet import stem
+        x = stem(x, m.RCNN_base[0], m.RCNN_base[1])
+    elif i == 3:
+        x = F.max_pool2d(x, 3, 2, 0, ceil_mode=True)
+    else:
+        for j, blk in enumerate(mod):
+            x = blk(x)
+            if not chk(f"base[{i}][{j}]", x):
+                sys.exit(1)
+    chk(f"base[{i}]", x)
+score, sr, prob, bbox = m.RCNN_rpn.head(x)
+for n, t in (("rpn score", score), ("rpn prob", prob), ("rpn bbox", bbox)):
+    chk(n, t)
+rois = m.RCNN_rpn.RPN_proposal((prob[:1].detach(), bbox[:1].detach(), b[1], "TRAIN"))
+chk("rois", rois)
+trois = m.RCNN_rpn.RPN_proposal((prob[1:].detach(), bbox[1:].detach(), b[6], "TEST"))
+chk("tgt rois", trois)
+print("rois min/max", rois[..., 1:].min().item(), rois[..., 1:].max().item(), flush=True)
+out = m.RCNN_proposal_target(rois, b[2], b[3])
+chk("sampled rois", out[0])
+pooled = m._pool(x[:1], out[0].view(-1, 5))
+chk("pooled", pooled)
+fc7 = m._head_to_tail(pooled)
+chk("fc7", fc7)
+ins, _ = m.RCNN_instanceDA(fc7, b[4])
+chk("ins", ins)
+torch.cuda.synchronize()
+print("done")

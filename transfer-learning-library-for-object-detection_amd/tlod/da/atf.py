@@ -30,7 +30,9 @@ from ..config import cfg
 from ..detector.losses import smooth_l1_loss
 from ..rpn.rpn_head import _RPN
 from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, image_label
+from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
+from ..detector.vgg16 import VGG16_SPLITS
 
 
 def instance_label_f(n_rows, need_backprop, minibatch=256):
@@ -54,15 +56,20 @@ class _fasterRCNN(_DAFBase):
         self.RCNN_rpn_t = _RPN(self.dout_base_model)
         for p in self.RCNN_rpn_t.parameters():
             p.requires_grad = False
-        self.RCNN_imageDA_3 = _ImageDA(256)
-        self.RCNN_imageDA_4 = _ImageDA(512)
+        self.RCNN_imageDA_3 = _ImageDA(256)  # VGG conv3_3 / ResNet layer1: 256 channels
+        self.RCNN_imageDA_4 = _ImageDA(512)  # VGG conv4_3 / ResNet layer2: 512 channels
         self.RCNN_imageDA = _ImageDA(self.dout_base_model)
         self.RCNN_instanceDA = _InstanceDA(self.instance_dim)
 
+    def _shared(self, x):
+        """The frozen prefix both branches share (VGG16 conv1/conv2; ResNet conv1..layer1)."""
+        return self.RCNN_base[:self.splits[0]](x)
+
     def _branch(self, layers, z):
-        c3 = layers[10:16](z)
-        c4 = layers[16:23](c3)
-        return c3, c4, layers[23:](c4)
+        shared, e3, e4 = self.splits
+        c3 = layers[shared:e3](z) if e3 > shared else z
+        c4 = layers[e3:e4](c3)
+        return c3, c4, layers[e4:](c4)
 
     @staticmethod
     def _img_loss(score, need):
@@ -84,7 +91,7 @@ class _fasterRCNN(_DAFBase):
 
         # ---- backbones: frozen conv1/conv2 are shared by both branches (vgg16.py:46-47)
         if same:
-            z = self.RCNN_base[:10](torch.cat([im_data, tgt_im_data], 0))
+            z = self._shared(torch.cat([im_data, tgt_im_data], 0))
             c3s, c4s, bs = self._branch(self.RCNN_base, z)
             c3_t, c4_t, base_t = self._branch(self.RCNN_base_t, z[:1])
             base_feat, tgt_base_feat = bs[:1], bs[1:]
@@ -92,11 +99,10 @@ class _fasterRCNN(_DAFBase):
             heads = rpn.head(torch.cat([base_feat, base_t, tgt_base_feat], 0))
             hs = [tuple(h[i:i + 1] for h in heads) for i in range(3)]
         else:
-            z = self.RCNN_base[:10](im_data)
+            z = self._shared(im_data)
             _, _, base_feat = self._branch(self.RCNN_base, z)
             c3_t, c4_t, base_t = self._branch(self.RCNN_base_t, z)
-            tgt_c3, tgt_c4, tgt_base_feat = self._branch(self.RCNN_base,
-                                                         self.RCNN_base[:10](tgt_im_data))
+            tgt_c3, tgt_c4, tgt_base_feat = self._branch(self.RCNN_base, self._shared(tgt_im_data))
             hs = [rpn.head(f) for f in (base_feat, base_t, tgt_base_feat)]
 
         # ---- RPN, train mode, on the source image through both branches (:130-134)
@@ -201,14 +207,50 @@ class vgg16(_fasterRCNN):
         self.class_agnostic = class_agnostic
         _fasterRCNN.__init__(self, classes, class_agnostic)
 
+    splits = VGG16_SPLITS
+
     def _init_modules(self):
         _daf_vgg16._init_modules(self)
-        layers = list(self.RCNN_base)
-        self.RCNN_base_t = nn.Sequential(*(layers[:10] + [copy.deepcopy(m) for m in layers[10:]]))
-        lt = list(self.RCNN_base_t)
-        self.conv3_s, self.conv3_t = nn.Sequential(*layers[:16]), nn.Sequential(*lt[:16])
-        self.conv34_s, self.conv34_t = nn.Sequential(*layers[16:23]), nn.Sequential(*lt[16:23])
-        self.conv45_s, self.conv45_t = nn.Sequential(*layers[23:]), nn.Sequential(*lt[23:])
+        _make_t_branch(self)
 
     def _head_to_tail(self, pool5):
         return self.RCNN_top(pool5.view(pool5.size(0), -1))
+
+
+def _make_t_branch(m):
+    """RCNN_base_t: the frozen prefix shared, the rest deep-copied (vgg16.py:44-50), and
+    the conv3/conv34/conv45 _s/_t views (:52-59)."""
+    shared, e3, e4 = m.splits
+    layers = list(m.RCNN_base)
+    m.RCNN_base_t = type(m.RCNN_base)(*(layers[:shared] + [copy.deepcopy(x) for x in layers[shared:]]))
+    for tag, base in (("s", m.RCNN_base), ("t", m.RCNN_base_t)):
+        setattr(m, "conv3_" + tag, base[:e3])
+        setattr(m, "conv34_" + tag, base[e3:e4])
+        setattr(m, "conv45_" + tag, base[e4:])
+
+
+class resnet(_fasterRCNN):
+    """ATF with ResNet101.  The reference's lib/ATF/resnet.py cannot run (its forward needs
+    conv3_s/_t... which only ATF/vgg16.py defines): built here the way the
+    VGG16 variant is, with the taps conv1..layer1 | layer2 | layer3 (ATF/resnet.py:238-241),
+    the frozen conv1..layer1 shared and layer2/layer3 copied for the t branch, and the
+    instance head on the 2048-d features.  Parity is against the oracle restatement only."""
+
+    splits = None
+
+    def __init__(self, classes, num_layers=101, pretrained=False, class_agnostic=False):
+        if num_layers != 101:
+            raise NotImplementedError("only ResNet101")
+        self.dout_base_model = 1024
+        self.instance_dim = 2048
+        self.pretrained = pretrained
+        self.class_agnostic = class_agnostic
+        _fasterRCNN.__init__(self, classes, class_agnostic)
+
+    def _init_modules(self):
+        _daf_resnet._init_modules(self)
+        self.splits = self.RCNN_base.SPLITS
+        _make_t_branch(self)
+
+    train = _daf_resnet.train
+    _head_to_tail = _daf_resnet._head_to_tail

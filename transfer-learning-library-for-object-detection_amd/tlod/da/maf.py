@@ -19,7 +19,9 @@ import torch.nn.functional as F
 from .. import _lib
 from ..conv import Conv2d
 from .daf import _ImageDA, _fasterRCNN as _DAFBase, grad_reverse, image_label
+from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
+from ..detector.vgg16 import VGG16_SPLITS
 
 
 class SpaceToDepthFunction(torch.autograd.Function):
@@ -262,10 +264,36 @@ class vgg16(_fasterRCNN):
 
     def _init_modules(self):
         _daf_vgg16._init_modules(self)
-        layers = list(self.RCNN_base)
-        self.conv3 = nn.Sequential(*layers[:16])
-        self.conv34 = nn.Sequential(*layers[16:23])
-        self.conv45 = nn.Sequential(*layers[23:])
+        _make_taps(self, VGG16_SPLITS)
 
     def _head_to_tail(self, pool5):
         return self.RCNN_top(pool5.view(pool5.size(0), -1))
+
+
+def _make_taps(m, splits):
+    _, e3, e4 = splits
+    m.conv3, m.conv34, m.conv45 = m.RCNN_base[:e3], m.RCNN_base[e3:e4], m.RCNN_base[e4:]
+
+
+class resnet(_fasterRCNN):
+    """MAF with ResNet101.  lib/MAF/resnet.py builds RCNN_base but not the conv3 / conv34 /
+    conv45 taps its forward uses (lib/MAF/faster_rcnn.py:59-61), so it cannot run; built
+    here with the taps conv1..layer1 (256 ch) | layer2 (512) | layer3 (1024) — the channel
+    counts the MAF discriminators already expect (DRM(256,64,4), DRM(512,256,2)) — and the
+    instance head on [2048-d fc7 || cls_prob].  Parity is against the oracle only."""
+
+    def __init__(self, classes, num_layers=101, pretrained=False, class_agnostic=False):
+        if num_layers != 101:
+            raise NotImplementedError("only ResNet101")
+        self.dout_base_model = 1024
+        self.instance_dim = 2048
+        self.pretrained = pretrained
+        self.class_agnostic = class_agnostic
+        _fasterRCNN.__init__(self, classes, class_agnostic)
+
+    def _init_modules(self):
+        _daf_resnet._init_modules(self)
+        _make_taps(self, self.RCNN_base.SPLITS)
+
+    train = _daf_resnet.train
+    _head_to_tail = _daf_resnet._head_to_tail

@@ -133,15 +133,27 @@ class Bottleneck(nn.Module):
 
 
 class ResNetBase(nn.Sequential):
-    """RCNN_base = Sequential(conv1, bn1, relu, maxpool, layer1, layer2, layer3)."""
+    """RCNN_base = Sequential(conv1, bn1, relu, maxpool, layer1, layer2, layer3).  Slices
+    (MAF/ATF taps: [:5] conv1..layer1, [5:6] layer2, [6:] layer3) keep this forward."""
+
+    # split points (shared frozen prefix end, conv3 end, conv4 end) for the MAF / ATF taps
+    SPLITS = (5, 5, 6)
 
     def forward(self, x):
-        conv1, bn1, _, maxpool, *layers = list(self)
-        x = stem(x, conv1, bn1)
-        x = F.max_pool2d(x, maxpool.kernel_size, maxpool.stride, maxpool.padding,
-                         ceil_mode=maxpool.ceil_mode)
-        for layer in layers:
-            x = layer(x)
+        mods = list(self)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, nn.Conv2d):  # stem conv1 + bn1 + relu, fused
+                assert isinstance(mods[i + 1], nn.BatchNorm2d) and isinstance(mods[i + 2], nn.ReLU)
+                x = stem(x, m, mods[i + 1])
+                i += 3
+                continue
+            if isinstance(m, nn.MaxPool2d):
+                x = F.max_pool2d(x, m.kernel_size, m.stride, m.padding, ceil_mode=m.ceil_mode)
+            else:
+                x = m(x)
+            i += 1
         return x
 
 

@@ -10,6 +10,10 @@ import torch.nn as nn
 
 from ..conv import Conv2d, vgg_init_
 
+# split points (shared frozen prefix end, conv3 end, conv4 end) of RCNN_base for the MAF /
+# ATF taps: conv3 = features[:16], conv34 = [16:23], conv45 = [23:-1] (lib/MAF/vgg16.py:84-86)
+VGG16_SPLITS = (10, 16, 23)
+
 # torchvision vgg16 cfg "D"
 VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512]
 
