@@ -24,6 +24,22 @@ namespace tlod {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// These kernels run 1-2 workgroups of 8 waves per CU (LDS-bound), i.e. 2-4 waves per SIMD:
+// telling the register allocator so lets the scheduler hoist LDS operand reads ahead of
+// the MFMAs instead of minimising VGPRs for an occupancy the LDS never allows.
+#ifndef TLOD_CONV_PF
+#define TLOD_CONV_PF 2
+#endif
+#ifndef TLOD_CONV_SGB
+#define TLOD_CONV_SGB 4
+#endif
+#ifndef TLOD_CONV_SGB_W
+#define TLOD_CONV_SGB_W 0
+#endif
+#ifndef TLOD_CONV_OCC
+#define TLOD_CONV_OCC __attribute__((amdgpu_waves_per_eu(2, 4)))
+#endif
+
 // Out-of-range staging loads read this zero block instead of branching (a branch per
 // load makes hipcc wait vmcnt(0) after each one; a select after the load pins the wait
 // to the load instead of the LDS store that follows the MFMA phase).
@@ -78,7 +94,7 @@ struct FwdCfg {
 };
 
 template <int WM, int WN, int MI, int NJ, int CK, int KS, bool VEC4>
-__global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
+__global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
     const float* __restrict__ X, const float* __restrict__ Wk, Epi epi, float* __restrict__ Y,
     int N, int Cin, int H, int W, int Cout, int tiles_m, int tiles_w, int tiles_h, int dp_tiles,
     int ksplit, int cps, float* __restrict__ slab) {
@@ -236,19 +252,33 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_fwd_kernel(
     const float* Bl = Bs + b_base;
     const bool more = ch + 1 < c_end;
     if (more) load_chunk(ch + 1);
+    // operands of step kk+PF are read while step kk's MFMAs run (PF-deep register ring;
+    // every index is compile-time after unrolling)
+    constexpr int PF = TLOD_CONV_PF;
+    float a[PF + 1][MI], b[PF + 1][NJ];
+    auto read_ops = [&](int kk, float (&ar)[MI], float (&br)[NJ]) {
+      const int ci = kk / C::KK, s = kk % C::KK;
+      const int boff = (ci * C::PH + s / KS) * C::PW + s % KS;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) ar[i] = Al[kk * C::BM + i * 32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) br[j] = Bl[boff + j * C::PW];
+    };
+#pragma unroll
+    for (int kk = 0; kk < PF; ++kk) read_ops(kk, a[kk], b[kk]);
 #pragma unroll
     for (int kk = 0; kk < C::HALF; ++kk) {
-      const int ci = kk / C::KK, s = kk % C::KK;        // compile-time after unrolling
-      const int boff = (ci * C::PH + s / KS) * C::PW + s % KS;
-      float a[MI], b[NJ];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = Al[kk * C::BM + i * 32];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = Bl[boff + j * C::PW];
+      if (kk + PF < C::HALF) read_ops(kk + PF, a[(kk + PF) % (PF + 1)], b[(kk + PF) % (PF + 1)]);
+      const int q = kk % (PF + 1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[q][i], b[q][j], acc[i][j]);
+#if TLOD_CONV_SGB
+      // pin the interleave: this step's operand reads (for kk+PF) ahead of its MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, TLOD_CONV_SGB, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, MI * NJ, 0);
+#endif
     }
     if (more) {
       float* Ad = lds + ((it + 1) & 1) * (C::A_ELEMS + C::B_ELEMS);
@@ -330,7 +360,7 @@ struct WgCfg {
 };
 
 template <int WM, int WN, int MI, int NJ, int KS, int TH>
-__global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
+__global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_kernel(
     const float* __restrict__ G, const float* __restrict__ X, float* __restrict__ slab, int N,
     int Cin, int H, int W, int Cout, int tiles_m, int tiles_n, int splits, int chunks_per_split) {
   using C = WgCfg<WM, WN, MI, NJ, KS, TH>;
@@ -465,6 +495,10 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_wgrad_kernel(
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+#if TLOD_CONV_SGB_W
+      __builtin_amdgcn_sched_group_barrier(0x100, TLOD_CONV_SGB_W, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, MI * NJ, 0);
+#endif
     }
     if (more) {
       float* Gd = lds + ((it + 1) & 1) * BUF;

@@ -12,6 +12,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libtlod.so")
+if os.environ.get("TLOD_LIB"):  # tuning builds (tools/build_variants.sh); same ABI
+    LIB_PATH = os.environ["TLOD_LIB"]
 
 c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
 c_size_t, c_void_p, c_uint64 = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64
