@@ -70,6 +70,22 @@ def conv_roofline(records):
     return achieved, detail, tot_ms, tot_f, len(records)
 
 
+def measured_traffic(a):
+    """HBM bytes per conv call from the latest committed PMC passes (profiles/r*/
+    conv_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE over the conv
+    kernels of this same bench command); None for workloads it was not measured on."""
+    import glob
+    if (a.method, a.net, a.height, a.width) != ("daf", "vgg16", 600, 1200):
+        return None, None
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", "r*", "conv_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    return t["bytes_per_call"], os.path.relpath(files[-1], here)
+
+
 def cpu_baseline(steps, H, W):
     """The oracle's CPU DAF step (test-infrastructure restatement) on this host's cores."""
     import oracle.daf_step as ods
@@ -129,6 +145,7 @@ def main():
     last_loss = float(torch.stack(losses).float().mean().item())
 
     achieved, detail, conv_ms, conv_f, n_launch = conv_roofline(records)
+    traffic_bytes, traffic_src = measured_traffic(a)
     result = {
         "metric": METRIC.replace("DAF VGG16", f"{a.method.upper()} {'VGG16' if a.net == 'vgg16' else 'ResNet101'}"),
         "value": round(value, 4), "unit": "img/s", "n_gpus": world,
@@ -145,7 +162,8 @@ def main():
                    "rcnn_batch": 256 if a.net == "vgg16" else 128},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                      "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": traffic_bytes, "traffic_source": traffic_src,
                      "kernel": "tlod conv (fwd+dgrad+wgrad, f32 MFMA implicit GEMM)",
                      "launches": n_launch, "kernel_ms_per_step": round(conv_ms / a.steps, 3),
                      "gflop_per_step": round(conv_f / a.steps / 1e9, 2), "by_kind": detail},
