@@ -233,6 +233,27 @@ int tlod_conv_fwd_ex_f32(const float* x, const float* wk, const float* scale, co
 int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float* scale, float* g,
                          float* g_raw, float* db, int N, int C, int HW, tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ Split-bf16 3x3 conv
+ * The forward / dgrad of tlod_conv_fwd_f32 on the bf16 MFMA: each f32 operand is split
+ * exactly into three bf16 terms (x = hi + mid + lo, truncation) and nprod = 6 products
+ * (hi*hi, hi*mid, mid*hi, hi*lo, mid*mid, lo*hi) are accumulated in f32 — error at the
+ * level of f32 rounding (normwise ~1e-7 vs fp64, like the f32-input MFMA path) at up to
+ * 2.7x its MFMA rate; nprod = 3 (hi*hi, hi*mid, mid*hi) trades that for ~5e-6.
+ * Weights are packed (and pre-split) per weight version into three bf16 planes
+ * (hi, mid, lo): pack_bs(dgrad=0): P[pl][co][c*80 + s*8 + e] = split(weight[co][8c+e][s])[pl];
+ * pack_bs(dgrad=1): P[pl][ci][c*80 + s*8 + e] = split(weight[8c+e][ci][8-s])[pl] (zero for
+ * the pad tap s = 9 and past the last channel).  dgrad = tlod_conv_fwd_bs_f32(dy, P_dgrad, ..., Cin := Cout,
+ * Cout := Cin).  KS = 3 only. */
+size_t tlod_conv_pack_bs_bytes(int Cout, int Cin, int KS, int dgrad);
+int tlod_conv_pack_bs(const float* weight, int Cout, int Cin, int KS, int dgrad, void* packed,
+                      tlod_stream_t stream);
+size_t tlod_conv_fwd_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
+                                        int nprod);
+int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float* scale, const float* bias,
+                         const float* residual, float* y, int N, int Cin, int H, int W, int Cout,
+                         int KS, int relu, int nprod, void* ws, size_t ws_bytes,
+                         tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ ResNet101 extras
  * Replaces: cuDNN for the ResNet101 stem conv1 7x7/2 + bn1 + relu (lib/DAF/resnet.py:107-110,
  *   frozen, forward only) and the stride-2 1x1 convolutions of the caffe-style bottleneck

@@ -1,0 +1,92 @@
+"""Split-bf16 3x3 convolution (tlod_conv_fwd_bs_f32: f32 operands split exactly into three
+bf16 terms, products on the bf16 MFMA, f32 accumulation) vs a PyTorch fp64 CPU reference.
+
+Bars (normwise relative / elementwise vs max|ref|): bf16x6 — the same 1e-5 / 1e-4 bar as
+the f32-input MFMA path (measured error is f32-rounding level); bf16x3 — 5e-5 / 5e-4
+(dropped terms are ~2^-16 relative per product).  Forward (with the BN-fold / residual /
+ReLU epilogue) and dgrad, including the split-K tail schedule and ragged channel counts.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+BARS = {"bf16x6": (1e-5, 1e-4), "bf16x3": (5e-5, 5e-4)}
+
+
+def _close(got, ref, math):
+    tol, etol = BARS[math]
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    nrm = float((got - ref).norm() / max(float(ref.norm()), 1e-30))
+    assert nrm <= tol, f"{math}: normwise rel err {nrm:.3e}"
+    assert float((got - ref).abs().max()) <= etol * float(ref.abs().max()) + 1e-30
+    return nrm
+
+
+SHAPES = [  # N, Cin, Cout, H, W
+    (2, 64, 128, 37, 75), (1, 3, 64, 50, 70), (2, 256, 256, 30, 40), (1, 512, 512, 37, 62),
+    (1, 13, 20, 9, 33), (1, 130, 132, 9, 33), (1, 64, 256, 150, 250),
+]
+
+
+@pytest.mark.parametrize("math", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("N,Cin,Cout,H,W", SHAPES)
+def test_conv_bs_fwd_dgrad(math, N, Cin, Cout, H, W):
+    from tlod.conv import conv_dgrad, conv_fwd
+    g = torch.Generator().manual_seed(N * 1000 + Cin + Cout + H)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    y = conv_fwd(x.to(dev), w.to(dev), b.to(dev), relu=False, math=math)
+    _close(y, F.conv2d(x.double(), w.double(), b.double(), padding=1), math)
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    dx = conv_dgrad(gy.to(dev), w.to(dev), math=math)
+    _close(dx, torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=1), math)
+
+
+@pytest.mark.parametrize("math", ["bf16x6"])
+def test_conv_bs_epilogue(math):
+    from tlod.conv import conv_fwd
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 64, 19, 37, generator=g)
+    w = torch.randn(96, 64, 3, 3, generator=g) * 0.05
+    sc, sh = torch.rand(96, generator=g) + 0.5, torch.randn(96, generator=g)
+    r = torch.randn(2, 96, 19, 37, generator=g)
+    y = conv_fwd(x.to(dev), w.to(dev), sh.to(dev), relu=True, scale=sc.to(dev), residual=r.to(dev),
+                 math=math)
+    ref = F.relu(F.conv2d(x.double(), w.double(), padding=1) * sc.double().view(1, -1, 1, 1)
+                 + sh.double().view(1, -1, 1, 1) + r.double())
+    _close(y, ref, math)
+
+
+def test_conv_bs_matches_f32_path_closely():
+    """bf16x6 and the f32-input MFMA path agree to f32 rounding on a conv3_3 shape."""
+    from tlod.conv import conv_fwd
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 256, 75, 125, generator=g).to(dev)
+    w = (torch.randn(256, 256, 3, 3, generator=g) * 0.03).to(dev)
+    a = conv_fwd(x, w, None, False, math="f32")
+    b = conv_fwd(x, w, None, False, math="bf16x6")
+    assert float((a - b).norm() / a.norm()) < 1e-6
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 256, 256, 30, 40), (1, 64, 128, 75, 150)])
+def test_bf16x6_as_accurate_as_f32_mfma(N, Cin, Cout, H, W):
+    """The default split-bf16 math is no less accurate than the f32-input MFMA path: its
+    normwise error vs fp64 is within 1.5x of the f32 path's on the same data."""
+    from tlod.conv import conv_dgrad, conv_fwd
+    g = torch.Generator().manual_seed(Cin + H)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    ref_y = F.conv2d(x.double(), w.double(), padding=1)
+    ref_dx = torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=1)
+
+    def err(a, r):
+        return float((a.detach().double().cpu() - r).norm() / r.norm())
+    e = {m: (err(conv_fwd(x.to(dev), w.to(dev), None, False, math=m), ref_y),
+             err(conv_dgrad(gy.to(dev), w.to(dev), math=m), ref_dx)) for m in ("f32", "bf16x6")}
+    assert e["bf16x6"][0] <= 1.5 * e["f32"][0] + 1e-9, e
+    assert e["bf16x6"][1] <= 1.5 * e["f32"][1] + 1e-9, e

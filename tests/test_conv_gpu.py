@@ -28,8 +28,10 @@ SHAPES = [  # N, Cin, Cout, H, W, KS
 ]
 
 
+@pytest.mark.parametrize("math", ["f32", "bf16x6"])
 @pytest.mark.parametrize("N,Cin,Cout,H,W,KS", SHAPES)
-def test_conv_fwd_bwd(N, Cin, Cout, H, W, KS):
+def test_conv_fwd_bwd(N, Cin, Cout, H, W, KS, math, monkeypatch):
+    monkeypatch.setenv("TLOD_CONV_MATH", math)
     from tlod.conv import ConvFunction
     g = torch.Generator().manual_seed(N * 1000 + Cin + Cout + H)
     x = torch.randn(N, Cin, H, W, generator=g)
@@ -73,7 +75,13 @@ def test_wgrad_deterministic():
 
 @pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 512, 512, 37, 75), (1, 512, 512, 12, 20),
                                             (2, 256, 512, 38, 40), (1, 64, 256, 150, 250)])
-def test_conv_split_k_paths(N, Cin, Cout, H, W):
+@pytest.mark.parametrize("math", ["f32", "bf16x6"])
+def test_conv_split_k_paths(N, Cin, Cout, H, W, math, monkeypatch):
+    monkeypatch.setenv("TLOD_CONV_MATH", math)
+    _split_k_case(N, Cin, Cout, H, W)
+
+
+def _split_k_case(N, Cin, Cout, H, W):
     """Small maps split every tile over input channels; larger ones (the last shape: 608
     tiles on 512 slots) split only the tail round.  Both go through the slab + reduce."""
     from tlod import _lib

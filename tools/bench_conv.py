@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--W", type=int, default=250)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true", help="also time MIOpen fp32")
+    ap.add_argument("--math", default="f32", choices=tc.MATHS)
     a = ap.parse_args()
     dev = "cuda"
     N, C, H, W = a.N, a.C, a.H, a.W
@@ -44,11 +45,12 @@ def main():
     b = torch.zeros(C, device=dev)
     g = torch.randn(N, C, H, W, device=dev)
     flop = 2.0 * N * H * W * C * C * 9
-    wk = tc.pack_fwd(w)
-    wd = tc.pack_dgrad(w)
-    out = {}
-    out["fwd_ms"] = timeit(lambda: tc.conv_fwd(x, w, b, True, wk=wk), a.iters)
-    out["dgrad_ms"] = timeit(lambda: tc.conv_dgrad(g, w, wd=wd), a.iters)
+    m = a.math
+    wk = tc.pack_fwd(w) if m == "f32" else tc.pack_bs(w, False)
+    wd = tc.pack_dgrad(w) if m == "f32" else tc.pack_bs(w, True)
+    out = {"math": m}
+    out["fwd_ms"] = timeit(lambda: tc.conv_fwd(x, w, b, True, wk=wk, math=m), a.iters)
+    out["dgrad_ms"] = timeit(lambda: tc.conv_dgrad(g, w, wd=wd, math=m), a.iters)
     out["wgrad_ms"] = timeit(lambda: tc.conv_wgrad(g, x, 3), a.iters)
     for k in ("fwd", "dgrad", "wgrad"):
         out[k + "_tflops"] = flop / (out[k + "_ms"] * 1e-3) / 1e12

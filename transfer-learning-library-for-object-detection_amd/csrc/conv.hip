@@ -329,6 +329,321 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
     }
 }
 
+// ======================================================================= split-bf16 forward
+// The same implicit GEMM on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32-input
+// rate) with every f32 operand split exactly into three bf16 terms by truncation,
+// x = hi + mid + lo (hi keeps the top 8 mantissa bits, mid the next 8, lo the last 8; the
+// remainders are exact in f32).  NP = 6 accumulates lo*hi, mid*mid, hi*lo, mid*hi, hi*mid,
+// hi*hi (the dropped terms are < 2^-24 relative: f32-level error; measured normwise error
+// vs fp64 ~1e-7, the same as the f32-input MFMA path); NP = 3 keeps the last three
+// (~5e-6).  Products of bf16 pairs are exact in the f32 accumulator.
+//
+// KS = 3 only.  K order inside a chunk of 8 input channels is (tap, channel), and one
+// 32x32x16 MFMA step covers two taps: lanes 0-31 take tap 2s, lanes 32-63 tap 2s+1 (step 4
+// pairs tap 8 with a zero-weight pad tap), each reading its 8 channels as 16 contiguous
+// bytes per plane.  Operands are split ONCE, when staged: the weights are pre-split in
+// global memory (pack_bs_kernel, per weight version) and copied plane by plane; the input
+// patch is split by the thread that stages it (one position x 8 channels) and stored as
+// bf16 planes [pos][8 ch].  Weight rows use a 176-B pitch so the 16-lane ds_read_b128
+// groups are conflict-free; patch positions are 16 B apart (conflict-free as is).
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned pack_hi2(unsigned lo_elem, unsigned hi_elem) {
+  return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);  // upper halves -> 2 x bf16
+}
+
+// split 8 floats into NPL bf16 planes (16 B each)
+template <int NPL>
+__device__ __forceinline__ void split8(const float (&v)[8], u32x4 (&out)[3]) {
+  unsigned hb[8], mb[8], lb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const unsigned u = __float_as_uint(v[e]);
+    hb[e] = u & 0xffff0000u;
+    const float r = v[e] - __uint_as_float(hb[e]);
+    mb[e] = __float_as_uint(r) & 0xffff0000u;
+    if constexpr (NPL == 3) lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    out[0][q] = pack_hi2(hb[2 * q], hb[2 * q + 1]);
+    out[1][q] = pack_hi2(mb[2 * q], mb[2 * q + 1]);
+    if constexpr (NPL == 3) out[2][q] = pack_hi2(lb[2 * q], lb[2 * q + 1]);
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+constexpr int kBsKP = 80;  // packed k per chunk: 10 taps (9 + zero pad) x 8 channels
+
+template <int WM, int WN, int MI, int NJ, int NP>
+struct BsCfg {
+  static constexpr int NPL = NP == 6 ? 3 : 2;   // bf16 planes used
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * MI * 32;
+  static constexpr int TH = WN * NJ, TW = 32;
+  static constexpr int PH = TH + 2, PW = TW + 2, PP = PH * PW;
+  static constexpr int CK = 8;
+  static constexpr int STEPS = 5;               // tap pairs (0,1) (2,3) (4,5) (6,7) (8,pad)
+  static constexpr int AROW = 176;              // bytes per weight row per plane (160 used)
+  static constexpr int A_PLANE = BM * AROW;     // bytes
+  static constexpr int B_PLANE = PP * 16;       // bytes
+  static constexpr int BUF = NPL * (A_PLANE + B_PLANE);
+  static constexpr int LDS_BYTES = 2 * BUF + 2 * BM * 4;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int WM, int WN, int MI, int NJ, int NP>
+__global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
+    const float* __restrict__ X, const unsigned short* __restrict__ Wp, Epi epi,
+    float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int tiles_m, int tiles_w,
+    int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab) {
+  using C = BsCfg<WM, WN, MI, NJ, NP>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int n_tiles = tiles_m * tiles_w * tiles_h * N;
+  const int n_tail = n_tiles - dp_tiles;
+  const bool direct = (int)blockIdx.x < dp_tiles;
+  int t, split = 0, ti = 0;
+  if (direct) {
+    t = xcd_remap(blockIdx.x, dp_tiles);
+  } else {
+    const int u = xcd_remap(blockIdx.x - dp_tiles, n_tail * ksplit);
+    ti = u % n_tail;
+    split = u / n_tail;
+    t = dp_tiles + ti;
+  }
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int tw = t % tiles_w; t /= tiles_w;
+  const int th = t % tiles_h; t /= tiles_h;
+  const int n = t;
+  const int m0 = mt * C::BM, w0 = tw * C::TW, h0 = th * C::TH;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l32 = lane & 31, khalf = lane >> 5;
+
+  const float* Xn = X + (size_t)n * Cin * H * W;
+  const int nchunks = (Cin + C::CK - 1) / C::CK;
+  const size_t wrow = (size_t)nchunks * kBsKP;       // packed row length (bf16)
+  const size_t wplane = (size_t)Cout * wrow;         // packed plane length (bf16)
+
+  // ---- operand byte offsets inside one LDS buffer
+  const int a_base = (wm * MI * 32 + l32) * C::AROW + 16 * khalf;
+  int b_off[C::STEPS];
+#pragma unroll
+  for (int st = 0; st < C::STEPS; ++st) {
+    const int tap = min(2 * st + khalf, 8);
+    b_off[st] = C::NPL * C::A_PLANE + ((wn * NJ + tap / 3) * C::PW + l32 + tap % 3) * 16;
+  }
+
+  // ---- staging.  A: NPL planes x BM rows x 10 16-B segments; B: PP positions x 8 ch.
+  constexpr int A_SEG = kBsKP / 8;                   // 16-B segments per row per chunk
+  constexpr int A_N = C::NPL * C::BM * A_SEG;
+  constexpr int A_IT = (A_N + C::NT - 1) / C::NT;
+  constexpr int B_IT = (C::PP + C::NT - 1) / C::NT;
+  int a_lds[A_IT];
+  unsigned a_gl[A_IT];  // element offsets of the chunk-0 segment (planes < 2^31 elements)
+  unsigned a_valid = 0;
+#pragma unroll
+  for (int i = 0; i < A_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    const int pl = idx / (C::BM * A_SEG), rem = idx % (C::BM * A_SEG);
+    const int row = rem / A_SEG, q = rem % A_SEG;
+    const bool ok = idx < A_N && m0 + row < Cout;
+    a_valid |= (unsigned)ok << i;
+    a_lds[i] = idx < A_N ? pl * C::A_PLANE + row * C::AROW + 16 * q : -1;
+    a_gl[i] = ok ? (unsigned)(pl * wplane + (size_t)(m0 + row) * wrow + 8 * q) : 0u;
+  }
+  int b_pos[B_IT], b_goff[B_IT];
+  unsigned b_pvalid = 0;
+  const int HWi = H * W;
+#pragma unroll
+  for (int i = 0; i < B_IT; ++i) {
+    const int pos = tid + i * C::NT;
+    const int r = pos / C::PW, c = pos % C::PW;
+    const int gh = h0 - 1 + r, gw = w0 - 1 + c;
+    const bool ok = pos < C::PP && gh >= 0 && gh < H && gw >= 0 && gw < W;
+    b_pvalid |= (unsigned)ok << i;
+    b_pos[i] = pos < C::PP ? C::NPL * C::A_PLANE + pos * 16 : -1;
+    b_goff[i] = ok ? gh * W + gw : 0;
+  }
+  u32x4 ra[A_IT];
+  float rb[B_IT][8];
+  int nvalid = 0;  // input channels present in the staged chunk (uniform)
+
+  // Loads are unconditional with 32-bit offsets from uniform per-chunk bases (invalid
+  // positions read offset 0, channels past Cin re-read the last channel); validity is
+  // applied when storing to LDS (see conv_fwd_kernel: a branch per load serialises them).
+  auto load_chunk = [&](int ch) {
+    const unsigned short* Wc = Wp + (size_t)ch * kBsKP;
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i)
+      ra[i] = *reinterpret_cast<const u32x4*>(Wc + a_gl[i]);
+    const int ci0 = ch * C::CK;
+    nvalid = min(C::CK, Cin - ci0);
+    const float* Xc = Xn + (size_t)ci0 * HWi;
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rb[i][e] = Xc[min(e, nvalid - 1) * HWi + b_goff[i]];
+  };
+  auto store_chunk = [&](unsigned char* buf) {
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i)
+      if (a_lds[i] >= 0)
+        *reinterpret_cast<u32x4*>(buf + a_lds[i]) = ((a_valid >> i) & 1) ? ra[i] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      if (b_pos[i] < 0) continue;
+      float v[8];
+      const bool pv = (b_pvalid >> i) & 1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (pv && e < nvalid) ? rb[i][e] : 0.f;
+      u32x4 sp[3];
+      split8<C::NPL>(v, sp);
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        *reinterpret_cast<u32x4*>(buf + b_pos[i] + pl * C::B_PLANE) = sp[pl];
+    }
+  };
+
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float* bias_s = reinterpret_cast<float*>(smem + 2 * C::BUF);
+  float* scale_s = bias_s + C::BM;
+  if (tid < C::BM) {
+    const int co = min(m0 + tid, Cout - 1);
+    bias_s[tid] = epi.bias ? epi.bias[co] : 0.f;
+    scale_s[tid] = epi.scale ? epi.scale[co] : 1.f;
+  }
+  const int c_begin = direct ? 0 : split * cps;
+  const int c_end = direct ? nchunks : min(nchunks, c_begin + cps);
+  if (c_begin < c_end) {
+    load_chunk(c_begin);
+    store_chunk(smem);
+  }
+  __syncthreads();
+
+  for (int ch = c_begin; ch < c_end; ++ch) {
+    const int it = ch - c_begin;
+    const unsigned char* buf = smem + (it & 1) * C::BUF;
+    const bool more = ch + 1 < c_end;
+    if (more) load_chunk(ch + 1);
+#pragma unroll
+    for (int st = 0; st < C::STEPS; ++st) {
+      u32x4 a[MI][3], b[NJ][3];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int pl = 0; pl < C::NPL; ++pl)
+          a[i][pl] = *reinterpret_cast<const u32x4*>(buf + a_base + pl * C::A_PLANE +
+                                                     i * 32 * C::AROW + 32 * st);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int pl = 0; pl < C::NPL; ++pl)
+          b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_off[st] + pl * C::B_PLANE +
+                                                     j * C::PW * 16);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (NP == 6) {
+            acc[i][j] = mfma_bf16(a[i][2], b[j][0], acc[i][j]);
+            acc[i][j] = mfma_bf16(a[i][1], b[j][1], acc[i][j]);
+            acc[i][j] = mfma_bf16(a[i][0], b[j][2], acc[i][j]);
+          }
+          acc[i][j] = mfma_bf16(a[i][1], b[j][0], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[i][0], b[j][1], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[i][0], b[j][0], acc[i][j]);
+        }
+    }
+    if (more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
+    __syncthreads();
+  }
+
+  // epilogue (identical to conv_fwd_kernel)
+  constexpr int TP = C::TH * C::TW;
+  if (!direct) {
+    float* St = slab + ((size_t)split * n_tail + ti) * C::BM * TP;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+          St[ml * TP + (wn * NJ + j) * C::TW + l32] = acc[i][j][r];
+        }
+    return;
+  }
+  float* Yn = Y + (size_t)n * Cout * H * W;
+  const float* Rn = epi.residual ? epi.residual + (size_t)n * Cout * H * W : nullptr;
+  const bool has_scale = epi.scale != nullptr;
+  const int w = w0 + l32;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int h = h0 + wn * NJ + j;
+      if (h >= H || w >= W) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int co = m0 + ml;
+        if (co < Cout) {
+          const size_t idx = ((size_t)co * H + h) * W + w;
+          float v = acc[i][j][r];
+          if (has_scale) v *= scale_s[ml];
+          v += bias_s[ml];
+          if (Rn) v += Rn[idx];
+          if (epi.relu) v = fmaxf(v, 0.f);
+          Yn[idx] = v;
+        }
+      }
+    }
+}
+
+// Packed, pre-split weights for conv_fwd_bs_kernel: three bf16 planes (hi, mid, lo of the
+// exact truncation split), each P[pl][o][c*80 + s*8 + e] = weight of output row o, input
+// channel c*8+e, tap s (0 for s = 9 — the pad tap — and past the last channel).  dgrad = 1
+// packs the transposed, flipped operand (rows = input channels, inputs = output channels,
+// tap 8-s).
+__global__ void pack_bs_kernel(const float* __restrict__ Wt, unsigned short* __restrict__ P,
+                               int rows, int ins, int nchunks, int dgrad) {
+  const size_t rowlen = (size_t)nchunks * kBsKP;
+  const size_t plane = (size_t)rows * rowlen;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < plane;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int o = (int)(i / rowlen);
+    const int k = (int)(i % rowlen);
+    const int e = k % 8, s = (k / 8) % 10, c = k / kBsKP;
+    const int in = c * 8 + e;
+    float v = 0.f;
+    if (in < ins && s < 9)
+      v = dgrad ? Wt[((size_t)in * rows + o) * 9 + (8 - s)] : Wt[((size_t)o * ins + in) * 9 + s];
+    const unsigned u = __float_as_uint(v);
+    const unsigned hb = u & 0xffff0000u;
+    const float r = v - __uint_as_float(hb);
+    const unsigned mb = __float_as_uint(r) & 0xffff0000u;
+    const unsigned lb = __float_as_uint(r - __uint_as_float(mb));
+    P[i] = (unsigned short)(hb >> 16);
+    P[plane + i] = (unsigned short)(mb >> 16);
+    P[2 * plane + i] = (unsigned short)(lb >> 16);
+  }
+}
+
 // ======================================================================= wgrad
 // Block tile: BM = WM*MI*32 output channels x BN = WN*NJ*32 GEMM columns n=(ci,kh,kw);
 // K = pixels, chunked as TH=2 rows x 32 columns.  The MFMA pairs pixel (0, c) with
@@ -798,6 +1113,76 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, Epi epi, float* Y,
   return kUnsupported;
 }
 
+// ---- split-bf16 forward launch (KS = 3)
+template <int WM, int WN, int MI, int NJ, int NP>
+static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout) {
+  using C = BsCfg<WM, WN, MI, NJ, NP>;
+  static const int slots = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP>, C::NT,
+                                          C::LDS_BYTES);
+  const int nchunks = div_up(Cin, C::CK);
+  // cost model in f32-MFMA-equivalent time: the split products run ~16/NP x faster
+  return plan_schedule(div_up(Cout, C::BM), div_up(W, C::TW), div_up(H, C::TH), N, nchunks,
+                       2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
+                       C::BM * C::TH * C::TW, slots);
+}
+
+template <int WM, int WN, int MI, int NJ, int NP>
+static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, float* Y, int N,
+                         int Cin, int H, int W, int Cout, float* slab, size_t slab_bytes,
+                         hipStream_t s) {
+  using C = BsCfg<WM, WN, MI, NJ, NP>;
+  const FwdPlan p = plan_fwd_bs<WM, WN, MI, NJ, NP>(N, Cin, H, W, Cout);
+  const long long nwg = (long long)p.dp_tiles + (long long)p.n_tail() * (p.ksplit > 1 ? p.ksplit : 0);
+  TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
+  if (p.ksplit > 1 && slab_bytes < p.slab_bytes(C::BM, C::TH)) {
+    set_error("tlod_conv_bs: workspace too small for split-K");
+    return kWorkspace;
+  }
+  const size_t lds = C::LDS_BYTES;
+  auto kern = conv_fwd_bs_kernel<WM, WN, MI, NJ, NP>;
+  static bool attr = false;
+  if (!attr) {
+    TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wp, epi, Y, N, Cin, H, W,
+                     Cout, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps, slab);
+  TLOD_LAUNCH_CHECK();
+  if (p.ksplit > 1) {
+    const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
+    hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
+                       p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
+                       p.tiles_h, epi, Cout, H, W, Y);
+    TLOD_LAUNCH_CHECK();
+  }
+  return kOk;
+}
+
+static int conv_fwd_bs_dispatch(const float* X, const unsigned short* Wp, Epi epi, float* Y,
+                                int N, int Cin, int H, int W, int Cout, int KS, int nprod,
+                                float* slab, size_t sb, hipStream_t s, size_t* ws_query = nullptr) {
+  if (KS != 3) {
+    set_error("conv_bs: only 3x3 kernels");
+    return kUnsupported;
+  }
+  if (nprod != 3 && nprod != 6) {
+    set_error("conv_bs: nprod must be 3 or 6");
+    return kInvalidArg;
+  }
+#define TLOD_BS_CFG(WM_, WN_, MI_, NJ_, NP_)                                                    \
+  do {                                                                                          \
+    if (ws_query) {                                                                             \
+      using C_ = BsCfg<WM_, WN_, MI_, NJ_, NP_>;                                                \
+      *ws_query = plan_fwd_bs<WM_, WN_, MI_, NJ_, NP_>(N, Cin, H, W, Cout).slab_bytes(C_::BM, C_::TH); \
+      return kOk;                                                                               \
+    }                                                                                           \
+    return launch_fwd_bs<WM_, WN_, MI_, NJ_, NP_>(X, Wp, epi, Y, N, Cin, H, W, Cout, slab, sb, s); \
+  } while (0)
+  if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6);
+  TLOD_BS_CFG(1, 8, 2, 2, 3);
+#undef TLOD_BS_CFG
+}
+
 // Split count over pixel chunks: the weight-gradient tiles alone (Cout/128 x 9Cin/256 =
 // 18 for conv3_3) cannot fill the chip, so the reduction over pixels is split into slabs.
 // Pick the count whose grid best fills whole rounds of resident workgroups (a grid of
@@ -969,4 +1354,43 @@ extern "C" int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float
                      scale, g, g_raw, db, C, HW);
   TLOD_LAUNCH_CHECK();
   return kOk;
+}
+
+extern "C" size_t tlod_conv_pack_bs_bytes(int Cout, int Cin, int KS, int dgrad) {
+  if (KS != 3) return 0;
+  const int rows = dgrad ? Cin : Cout, ins = dgrad ? Cout : Cin;
+  return 3 * (size_t)rows * div_up(ins, 8) * kBsKP * sizeof(unsigned short);
+}
+
+extern "C" int tlod_conv_pack_bs(const float* weight, int Cout, int Cin, int KS, int dgrad,
+                                 void* packed, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(Cout > 0 && Cin > 0 && weight && packed, "bad arguments");
+  TLOD_CHECK_ARG(KS == 3, "split-bf16 conv: 3x3 only");
+  const int rows = dgrad ? Cin : Cout, ins = dgrad ? Cout : Cin;
+  const size_t plane = (size_t)rows * div_up(ins, 8) * kBsKP;
+  hipLaunchKernelGGL(pack_bs_kernel, dim3((unsigned)std::min<size_t>((plane + 255) / 256, 4096)),
+                     dim3(256), 0, (hipStream_t)stream, weight, (unsigned short*)packed, rows, ins,
+                     div_up(ins, 8), dgrad);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" size_t tlod_conv_fwd_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
+                                                   int nprod) {
+  size_t b = 0;
+  if (conv_fwd_bs_dispatch(nullptr, nullptr, Epi{}, nullptr, N, Cin, H, W, Cout, KS, nprod,
+                           nullptr, 0, nullptr, &b) != kOk)
+    return 0;
+  return b;
+}
+
+extern "C" int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float* scale,
+                                    const float* bias, const float* residual, float* y, int N,
+                                    int Cin, int H, int W, int Cout, int KS, int relu, int nprod,
+                                    void* ws, size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
+  TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
+  return conv_fwd_bs_dispatch(x, (const unsigned short*)wp, Epi{scale, bias, residual, relu}, y,
+                              N, Cin, H, W, Cout, KS, nprod, (float*)ws, ws_bytes,
+                              (hipStream_t)stream);
 }

@@ -88,6 +88,12 @@ SIGNATURES = {
     "tlod_conv_fwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, P, c_size_t, P]),
     "tlod_relu_bwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, P]),
+    "tlod_conv_pack_bs_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "tlod_conv_pack_bs": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_conv_fwd_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
+                                                    c_int]),
+    "tlod_conv_fwd_bs_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_int, c_int, P, c_size_t, P]),
     "tlod_stem_conv7x7s2_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),

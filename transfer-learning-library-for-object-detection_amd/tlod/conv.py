@@ -12,6 +12,7 @@ when the input does (conv3_1 of VGG16 needs no dgrad: its input comes from froze
 layers, lib/DAF/vgg16.py:52-53).
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -25,9 +26,10 @@ from . import _lib
 PROFILE = None
 
 
-def _timed(kind, shape, fn):
+def _timed(kind, shape, fn, math="f32"):
     if PROFILE is None:
         return fn()
+    kind = f"{kind}/{math}"
     N, Cin, H, W, Cout, KS = shape
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -35,6 +37,38 @@ def _timed(kind, shape, fn):
     e.record()
     PROFILE.append((s, e, 2.0 * N * H * W * Cout * Cin * KS * KS, kind, shape))
     return r
+
+
+MATHS = ("f32", "bf16x6", "bf16x3")
+
+
+def conv_math():
+    """Arithmetic of the 3x3 fwd/dgrad convolutions (env TLOD_CONV_MATH):
+      "bf16x6" (default): f32 operands split exactly into 3 bf16 terms, the 6 products down
+               to 2^-16 relative on the bf16 MFMA, f32 accumulation — f32-level error (the
+               same normwise ~1e-7 vs fp64 as the f32-input MFMA; tests/test_conv_bs_gpu.py);
+      "f32"  : the f32-input MFMA (exact f32 products);
+      "bf16x3": 3 products (~5e-6 normwise), opt-in.
+    1x1 convs and wgrad use the f32-input MFMA in every mode."""
+    m = os.environ.get("TLOD_CONV_MATH", "bf16x6")
+    if m not in MATHS:
+        raise ValueError(f"TLOD_CONV_MATH={m!r}: expected one of {MATHS}")
+    return m
+
+
+def _bs(KS, math):
+    return KS == 3 and math != "f32"
+
+
+def pack_bs(weight, dgrad):
+    """Pre-split bf16 planes of a 3x3 weight for the split-bf16 fwd (dgrad=0) / dgrad (1)."""
+    Cout, Cin, KS, _ = weight.shape
+    L = _lib.lib()
+    p = torch.empty(L.tlod_conv_pack_bs_bytes(Cout, Cin, KS, int(dgrad)), dtype=torch.uint8,
+                    device=weight.device)
+    _lib.check(L.tlod_conv_pack_bs(_lib.ptr(weight.detach().contiguous()), Cout, Cin, KS,
+                                   int(dgrad), _lib.ptr(p), _lib.stream_of(weight)), "pack_bs")
+    return p
 
 
 def _check(x, w):
@@ -61,12 +95,17 @@ def pack_dgrad(weight):
     return wd
 
 
-def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=None):
-    """y = act(conv(x, weight) * scale + bias + residual) (tlod_conv_fwd_ex_f32)."""
+def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=None, math=None):
+    """y = act(conv(x, weight) * scale + bias + residual) (tlod_conv_fwd_ex_f32, or
+    tlod_conv_fwd_bs_f32 for 3x3 under a split-bf16 math; wk: the matching pack)."""
     _check(x, weight)
     x = x.contiguous()
     N, Cin, H, W = x.shape
     Cout, _, KS, _ = weight.shape
+    math = conv_math() if math is None else math
+    if _bs(KS, math):
+        return _conv_bs(x, pack_bs(weight, False) if wk is None else wk, bias, relu, scale,
+                        residual, Cout, KS, math, "fwd")
     wk = pack_fwd(weight) if wk is None else wk
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
@@ -83,10 +122,33 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=Non
     return y
 
 
-def conv_dgrad(g, weight, wd=None):
+def _conv_bs(x, wp, bias, relu, scale, residual, Cout, KS, math, kind):
+    N, Cin, H, W = x.shape
+    y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
+    b = bias.detach().contiguous() if bias is not None else None
+    sc = scale.detach().contiguous() if scale is not None else None
+    res = residual.detach().contiguous() if residual is not None else None
+    L = _lib.lib()
+    nprod = 6 if math == "bf16x6" else 3
+    ws = _lib.workspace(L.tlod_conv_fwd_bs_workspace_bytes(N, Cin, H, W, Cout, KS, nprod), x.device,
+                        "conv")
+    shape = (N, Cin, H, W, Cout, KS) if kind == "fwd" else (N, Cout, H, W, Cin, KS)
+    _timed(kind, shape, lambda: _lib.check(
+        L.tlod_conv_fwd_bs_f32(_lib.ptr(x), _lib.ptr(wp), _lib.ptr(sc), _lib.ptr(b), _lib.ptr(res),
+                               _lib.ptr(y), N, Cin, H, W, Cout, KS, int(relu), nprod, _lib.ptr(ws),
+                               ws.numel(), _lib.stream_of(x)), "conv_fwd_bs"), math)
+    return y
+
+
+def conv_dgrad(g, weight, wd=None, math=None):
     g = g.contiguous()
     N, Cout, H, W = g.shape
     _, Cin, KS, _ = weight.shape
+    math = conv_math() if math is None else math
+    if _bs(KS, math):
+        # dgrad = the forward form over dy with the transposed, flipped pack
+        return _conv_bs(g, pack_bs(weight, True) if wd is None else wd, None, False, None, None,
+                        Cin, KS, math, "dgrad")
     wd = pack_dgrad(weight) if wd is None else wd
     dx = torch.empty((N, Cin, H, W), dtype=torch.float32, device=g.device)
     L = _lib.lib()
