@@ -253,6 +253,14 @@ int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float* scale, con
                          const float* residual, float* y, int N, int Cin, int H, int W, int Cout,
                          int KS, int relu, int nprod, void* ws, size_t ws_bytes,
                          tlod_stream_t stream);
+/* Split-bf16 wgrad: tlod_conv_wgrad_f32's result (same argument meaning, same
+ * deterministic split-K slab reduction) with dy and x split into bf16 planes on the fly and
+ * nprod (6 or 3) products on the bf16 MFMA.  No weight pack.  KS = 1 or 3. */
+size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
+                                          int nprod);
+int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, int accumulate, int N,
+                           int Cin, int H, int W, int Cout, int KS, int nprod, void* ws,
+                           size_t ws_bytes, tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ ResNet101 extras
  * Replaces: cuDNN for the ResNet101 stem conv1 7x7/2 + bn1 + relu (lib/DAF/resnet.py:107-110,

@@ -51,13 +51,17 @@ def main():
     out = {"math": m}
     out["fwd_ms"] = timeit(lambda: tc.conv_fwd(x, w, b, True, wk=wk, math=m), a.iters)
     out["dgrad_ms"] = timeit(lambda: tc.conv_dgrad(g, w, wd=wd, math=m), a.iters)
-    out["wgrad_ms"] = timeit(lambda: tc.conv_wgrad(g, x, 3), a.iters)
+    out["wgrad_ms"] = timeit(lambda: tc.conv_wgrad(g, x, 3, math=m), a.iters)
+    if m != "f32":
+        out["wgrad_f32_ms"] = timeit(lambda: tc.conv_wgrad(g, x, 3, math="f32"), a.iters)
     for k in ("fwd", "dgrad", "wgrad"):
         out[k + "_tflops"] = flop / (out[k + "_ms"] * 1e-3) / 1e12
     bwd = out["dgrad_ms"] + out["wgrad_ms"]
     out["bwd_gflop"] = 2 * flop / 1e9
     out["bwd_tflops"] = 2 * flop / (bwd * 1e-3) / 1e12
     out["bwd_frac_f32_mfma_peak"] = out["bwd_tflops"] / 157.3
+    if m != "f32":  # f32-equivalent peak of the split products
+        out["bwd_frac_split_peak"] = out["bwd_tflops"] / (2516.6 / int(m[-1]))
     if a.torch:
         xr = x.clone().requires_grad_(True)
         wr = w.clone().requires_grad_(True)

@@ -838,6 +838,274 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_kernel(
     }
 }
 
+// ------------------------------------------------------------ split-bf16 wgrad
+// The same GEMM on the bf16 MFMA (v_mfma_f32_32x32x16_bf16) with both operands split
+// exactly into NPL bf16 planes at staging time (as conv_fwd_bs_kernel), NP products per
+// f32 product.  K = pixels, flattened per image (p = h*W + w), so narrow maps waste no
+// MFMA lanes on row padding; a chunk is TK = 16 consecutive pixels = one MFMA k-step.
+// Both operands are staged K-contiguous ([row][16 px] bf16 per plane): A = dY rows (co),
+// B = the im2col rows (ci,kh,kw), element p of B-row (ci,kh,kw) = X[ci][p + (kh-pad)*W +
+// (kw-pad)] when that tap lies inside the map (else 0).
+//
+// Staging is VALU-lean because VALU, not MFMA, bounds a split-operand kernel: each lane
+// owns one 4-pixel segment of two A rows and two B rows and fetches each with ONE raw
+// buffer_load_dwordx4 (unaligned is fine; the per-dword range check zero-fills the tail of
+// the tensor and rows past Cout / columns past Cin*KS*KS, which read at offset 2^31).  The
+// in-map mask of a B segment is a few bit-range ops from (h, w) of its first pixel (one
+// float-reciprocal division per chunk, shared by all four segments).  A B segment starting
+// before the tensor (image 0, channel 0, first row: the dwordx4 would read all zeros) only
+// occurs in the first chunks of image 0, which take a per-dword load path (uniform branch).
+// Row pitch 48 B puts the 16 rows a ds_read_b128 lane group reads on 16 distinct 16-B
+// slots of the 256-B bank row (3r mod 16).  256x256 tiles (8 waves, 4x2 accumulators of
+// 32x32 each) give each staged element 256 uses.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ f32x4v raw_buffer_load_v4f32(i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ float raw_buffer_load_f32(i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.f32");
+
+__device__ __forceinline__ i32x4 make_buffer_rsrc(const void* p, unsigned bytes) {
+  struct __attribute__((packed)) R {
+    const void* ptr;
+    unsigned range;
+    unsigned config;
+  } r{p, bytes, 0x00020000u};
+  return __builtin_bit_cast(i32x4, r);
+}
+
+constexpr int kBufOOB = (int)0x80000000;  // voffset past any range: the load returns 0
+
+// bits [0, x) of a 4-bit mask, x clamped to [0, 4]
+__device__ __forceinline__ unsigned lt_mask4(int x) { return (1u << min(max(x, 0), 4)) - 1u; }
+
+// split 4 floats into NPL bf16 planes (8 B each)
+template <int NPL>
+__device__ __forceinline__ void split4(const float (&v)[4], unsigned (&out)[3][2]) {
+  unsigned hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const unsigned u = __float_as_uint(v[e]);
+    hb[e] = u & 0xffff0000u;
+    const float r = v[e] - __uint_as_float(hb[e]);
+    mb[e] = __float_as_uint(r) & 0xffff0000u;
+    if constexpr (NPL == 3) lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    out[0][q] = pack_hi2(hb[2 * q], hb[2 * q + 1]);
+    out[1][q] = pack_hi2(mb[2 * q], mb[2 * q + 1]);
+    if constexpr (NPL == 3) out[2][q] = pack_hi2(lb[2 * q], lb[2 * q + 1]);
+  }
+}
+
+template <int WM, int WN, int MI, int NJ, int NP>
+struct WgBsCfg {
+  static constexpr int NPL = NP == 6 ? 3 : 2;
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * MI * 32;
+  static constexpr int BN = WN * NJ * 32;
+  static constexpr int TK = 16;                    // pixels per chunk (one k-step)
+  static constexpr int PITCH = 48;                 // bytes per row per plane (32 used)
+  static constexpr int A_PLANE = BM * PITCH;
+  static constexpr int B_PLANE = BN * PITCH;
+  static constexpr int BUF = NPL * (A_PLANE + B_PLANE);
+  static constexpr int LDS_BYTES = 2 * BUF;
+  static constexpr int ROWS_PER_IT = NT / 4;       // 4 segments of 4 px per row
+  static constexpr int A_IT = BM / ROWS_PER_IT, B_IT = BN / ROWS_PER_IT;
+  static_assert(BM % ROWS_PER_IT == 0 && BN % ROWS_PER_IT == 0, "staging");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int WM, int WN, int MI, int NJ, int KS, int NP>
+__global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kernel(
+    const float* __restrict__ G, const float* __restrict__ X, float* __restrict__ slab, int N,
+    int Cin, int H, int W, int Cout, int tiles_m, int tiles_n, int splits, int chunks_per_split,
+    float inv_w) {
+  using C = WgBsCfg<WM, WN, MI, NJ, NP>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int KK = KS * KS;
+
+  const int nwg = tiles_m * tiles_n * splits;
+  int t = xcd_remap(blockIdx.x, nwg);
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int nt = t % tiles_n;
+  const int split = t / tiles_n;
+  const int m0 = mt * C::BM, n0 = nt * C::BN;
+  const int Ktot = Cin * KK;
+  const int P = H * W;
+  const int cpi = (P + C::TK - 1) / C::TK;
+  const int total_chunks = N * cpi;
+  const int c_begin = split * chunks_per_split;
+  const int c_end = min(total_chunks, c_begin + chunks_per_split);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l32 = lane & 31, khalf = lane >> 5;
+
+  const i32x4 g_rsrc = make_buffer_rsrc(G, (unsigned)N * Cout * P * 4u);
+  const i32x4 x_rsrc = make_buffer_rsrc(X, (unsigned)N * Cin * P * 4u);
+
+  // ---- per-lane staging constants: segment s4..s4+3 of A rows / B rows tid/4 + i*NT/4
+  const int s4 = (tid & 3) * 4;
+  int a_off[C::A_IT], a_lds[C::A_IT];
+#pragma unroll
+  for (int i = 0; i < C::A_IT; ++i) {
+    const int row = (tid >> 2) + i * C::ROWS_PER_IT;
+    a_off[i] = m0 + row < Cout ? (m0 + row) * P + s4 : -1;  // -1: row past Cout
+    a_lds[i] = row * C::PITCH + 2 * s4;
+  }
+  int b_off[C::B_IT], b_lds[C::B_IT], b_dh[C::B_IT], b_dw[C::B_IT];
+#pragma unroll
+  for (int i = 0; i < C::B_IT; ++i) {
+    const int cl = (tid >> 2) + i * C::ROWS_PER_IT;
+    const int col = n0 + cl;
+    const bool ok = col < Ktot;
+    const int ci = ok ? col / KK : 0, s = ok ? col % KK : 0;
+    b_dh[i] = ok ? s / KS - KS / 2 : -(1 << 20);  // dead column: never in the map
+    b_dw[i] = s % KS - KS / 2;
+    b_off[i] = ok ? ci * P + b_dh[i] * W + b_dw[i] + s4 : s4;
+    b_lds[i] = C::NPL * C::A_PLANE + cl * C::PITCH + 2 * s4;
+  }
+  f32x4v ra[C::A_IT], rb[C::B_IT];
+  unsigned a_mask = 0, b_mask[C::B_IT];
+
+  auto load_chunk = [&](int c) {
+    const int n = c / cpi;
+    const int pc = (c - n * cpi) * C::TK;   // first pixel of the chunk
+    const int pb = pc + s4;                 // first pixel of this lane's segments
+    const int gbase = n * Cout * P + pc, xbase = n * Cin * P + pc;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i)
+      ra[i] = raw_buffer_load_v4f32(g_rsrc, a_off[i] >= 0 ? (gbase + a_off[i]) * 4 : kBufOOB, 0, 0);
+    if (n == 0 && pc <= W) {
+      // segments that may start before the tensor: per-dword loads, elements before the
+      // tensor (outside the map anyway) sent out of range.  The select also keeps the
+      // backend from merging the four loads back into one dwordx4 at the negative start.
+#pragma unroll
+      for (int i = 0; i < C::B_IT; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int o = xbase + b_off[i] + e;
+          rb[i][e] = raw_buffer_load_f32(x_rsrc, o >= 0 ? o * 4 : kBufOOB, 0, 0);
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C::B_IT; ++i)
+        rb[i] = raw_buffer_load_v4f32(x_rsrc, (xbase + b_off[i]) * 4, 0, 0);
+    }
+    // masks: pixels past the image (tail chunk), then the taps' in-map test
+    const unsigned tmask = lt_mask4(P - pb);
+    a_mask = tmask;
+    const int h0 = (int)fmaf((float)pb, inv_w, 0.5f * inv_w);  // floor((pb + 0.5) / W)
+    const int w0 = pb - h0 * W;
+    if (W >= 4) {
+      // the 4 pixels are (h0, w0 + e) for e < ew, then (h0 + 1, e - ew): one wrap at most
+      const int ew = W - w0;
+#pragma unroll
+      for (int i = 0; i < C::B_IT; ++i) {
+        const int dw = b_dw[i], dwp = max(dw, 0), dwn = max(-dw, 0);
+        const bool r0 = (unsigned)(h0 + b_dh[i]) < (unsigned)H;
+        const bool r1 = (unsigned)(h0 + 1 + b_dh[i]) < (unsigned)H;
+        const unsigned m0v = lt_mask4(ew - dwp) & ~lt_mask4(-w0 - dw);
+        const unsigned m1v = 0xfu & ~lt_mask4(ew + dwn);
+        b_mask[i] = ((r0 ? m0v : 0u) | (r1 ? m1v : 0u)) & tmask;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C::B_IT; ++i) {
+        unsigned m = 0;
+        int h = h0, w = w0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = (unsigned)(h + b_dh[i]) < (unsigned)H && (unsigned)(w + b_dw[i]) < (unsigned)W;
+          m |= (unsigned)ok << e;
+          if (++w == W) { w = 0; ++h; }
+        }
+        b_mask[i] = m & tmask;
+      }
+    }
+  };
+  auto store_seg = [&](unsigned char* dst, int plane_bytes, f32x4v r, unsigned m) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = ((m >> e) & 1) ? r[e] : 0.f;
+    unsigned sp[3][2];
+    split4<C::NPL>(v, sp);
+#pragma unroll
+    for (int pl = 0; pl < C::NPL; ++pl)
+      *reinterpret_cast<uint2*>(dst + pl * plane_bytes) = make_uint2(sp[pl][0], sp[pl][1]);
+  };
+  auto store_chunk = [&](unsigned char* buf) {
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) store_seg(buf + a_lds[i], C::A_PLANE, ra[i], a_mask);
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) store_seg(buf + b_lds[i], C::B_PLANE, rb[i], b_mask[i]);
+  };
+
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int a_rd = (wm * MI * 32 + l32) * C::PITCH + 16 * khalf;
+  const int b_rd = C::NPL * C::A_PLANE + (wn * NJ * 32 + l32) * C::PITCH + 16 * khalf;
+  if (c_begin < c_end) {
+    load_chunk(c_begin);
+    store_chunk(smem);
+  }
+  __syncthreads();
+  for (int c = c_begin; c < c_end; ++c) {
+    const int it = c - c_begin;
+    const unsigned char* buf = smem + (it & 1) * C::BUF;
+    const bool more = c + 1 < c_end;
+    if (more) load_chunk(c + 1);
+    u32x4 b[NJ][3];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_rd + pl * C::B_PLANE + j * 32 * C::PITCH);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      u32x4 a[3];
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        a[pl] = *reinterpret_cast<const u32x4*>(buf + a_rd + pl * C::A_PLANE + i * 32 * C::PITCH);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (NP == 6) {
+          acc[i][j] = mfma_bf16(a[2], b[j][0], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[1], b[j][1], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[0], b[j][2], acc[i][j]);
+        }
+        acc[i][j] = mfma_bf16(a[1], b[j][0], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0], b[j][1], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0], b[j][0], acc[i][j]);
+      }
+    }
+    if (more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
+    __syncthreads();
+  }
+
+  float* S = slab + (size_t)split * Cout * Ktot;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + wn * NJ * 32 + j * 32 + l32;
+      if (col >= Ktot) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        if (co < Cout) S[(size_t)co * Ktot + col] = acc[i][j][r];
+      }
+    }
+}
+
 // dW = (accumulate ? dW : 0) + sum_s slab[s], summed in split order (deterministic).
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, size_t count,
                                    float* __restrict__ out, int accumulate) {
@@ -1245,6 +1513,68 @@ static int wgrad_splits(int N, int Cin, int H, int W, int Cout, int KS) {
   return with_wgrad_cfg(KS, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
 }
 
+// Split count by cost: rounds x chunks per split x chunk time + the slab round trip
+// (sp writes + sp reads + 1 write of Cout*Ktot floats).  Small maps (conv5 / RPN at
+// 37x75) cannot afford the 16-64 splits that fill the chip on conv3.
+static int pick_splits_cost(long long tiles, int chunks, int slots, double chunk_s,
+                            double dw_bytes) {
+  int best = 1;
+  double best_t = 1e30;
+  const int smax = std::max(1, std::min(128, chunks / 4));
+  for (int sp = 1; sp <= smax; ++sp) {
+    const int cps = div_up(chunks, sp);
+    const int esp = div_up(chunks, cps);
+    const long long rounds = (tiles * esp + slots - 1) / slots;
+    const double t = (double)rounds * cps * chunk_s + (2.0 * esp + 1.0) * dw_bytes / 4e12;
+    if (t < best_t * 0.999) {
+      best_t = t;
+      best = esp;
+    }
+  }
+  return best;
+}
+
+template <int WM, int WN, int MI, int NJ, int KS, int NP>
+struct WgradBs {
+  using C = WgBsCfg<WM, WN, MI, NJ, NP>;
+  static int splits(int N, int Cin, int H, int W, int Cout) {
+    static const int slots =
+        resident_slots(conv_wgrad_bs_kernel<WM, WN, MI, NJ, KS, NP>, C::NT, C::LDS_BYTES);
+    const long long tiles = (long long)div_up(Cout, C::BM) * div_up(Cin * KS * KS, C::BN);
+    const int chunks = N * div_up(H * W, C::TK);
+    // bf16 MFMA time of one chunk per resident slot at ~50% of the dense peak
+    const double chunk_s = 2.0 * C::BM * C::BN * C::TK * NP / (2516.6e12 * 0.5 / slots);
+    return pick_splits_cost(tiles, chunks, slots, chunk_s, 4.0 * Cout * Cin * KS * KS);
+  }
+  static int launch(const float* G, const float* X, float* slab, int splits, int N, int Cin,
+                    int H, int W, int Cout, hipStream_t s) {
+    const int tiles_m = div_up(Cout, C::BM), tiles_n = div_up(Cin * KS * KS, C::BN);
+    const int total_chunks = N * div_up(H * W, C::TK);
+    const int cps = div_up(total_chunks, splits);
+    const long long nwg = (long long)tiles_m * tiles_n * splits;
+    TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
+    auto kern = conv_wgrad_bs_kernel<WM, WN, MI, NJ, KS, NP>;
+    static bool attr = false;
+    if (!attr) {
+      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), C::LDS_BYTES, s, G, X, slab, N, Cin,
+                       H, W, Cout, tiles_m, tiles_n, splits, cps, 1.0f / (float)W);
+    TLOD_LAUNCH_CHECK();
+    return kOk;
+  }
+};
+
+template <typename F>
+static int with_wgrad_bs_cfg(int KS, int nprod, F&& f) {
+  if (KS == 3 && nprod == 6) return f(WgradBs<2, 4, 4, 2, 3, 6>{});
+  if (KS == 3 && nprod == 3) return f(WgradBs<2, 4, 4, 2, 3, 3>{});
+  if (KS == 1 && nprod == 6) return f(WgradBs<2, 4, 4, 2, 1, 6>{});
+  if (KS == 1 && nprod == 3) return f(WgradBs<2, 4, 4, 2, 1, 3>{});
+  return -1;
+}
+
 }  // namespace tlod
 
 using namespace tlod;
@@ -1326,6 +1656,41 @@ extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, i
   }
   float* slab = static_cast<float*>(ws);
   const int st = with_wgrad_cfg(KS, [&](auto cfg) {
+    return cfg.launch(dy, x, slab, splits, N, Cin, H, W, Cout, s);
+  });
+  if (st) return st;
+  const size_t count = (size_t)Cout * Cin * KS * KS;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count / 4 + 255) / 256, 2048)),
+                     dim3(256), 0, s, slab, splits, count, dw, accumulate);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
+                                                     int nprod) {
+  const int sp = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
+  return sp > 0 ? (size_t)sp * Cout * Cin * KS * KS * sizeof(float) : 0;
+}
+
+extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, int accumulate,
+                                      int N, int Cin, int H, int W, int Cout, int KS, int nprod,
+                                      void* ws, size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
+  TLOD_CHECK_ARG((Cout * Cin * KS * KS) % 4 == 0, "Cout*Cin*KS*KS must be a multiple of 4");
+  TLOD_CHECK_ARG(KS == 1 || KS == 3, "conv wgrad: only 1x1 and 3x3 kernels");
+  TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "conv wgrad bs: nprod must be 3 or 6");
+  // 32-bit buffer byte offsets; exact float-reciprocal pixel -> (h, w) below 2^21 pixels
+  TLOD_CHECK_ARG((size_t)N * std::max(Cin, Cout) * H * W * 4 < (1ull << 31), "tensor too large");
+  TLOD_CHECK_ARG((size_t)H * W < (1u << 21), "map too large");
+  hipStream_t s = (hipStream_t)stream;
+  const int splits =
+      with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
+  if (ws_bytes < (size_t)splits * Cout * Cin * KS * KS * sizeof(float)) {
+    set_error("tlod_conv_wgrad_bs_f32: workspace too small");
+    return kWorkspace;
+  }
+  float* slab = static_cast<float*>(ws);
+  const int st = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) {
     return cfg.launch(dy, x, slab, splits, N, Cin, H, W, Cout, s);
   });
   if (st) return st;

@@ -159,7 +159,17 @@ def conv_dgrad(g, weight, wd=None, math=None):
     return dx
 
 
-def conv_wgrad(g, x, KS, out=None, accumulate=False):
+def wgrad_math():
+    """Arithmetic of the 3x3 weight gradients (env TLOD_WGRAD_MATH, default: the
+    TLOD_CONV_MATH choice): "bf16x6" / "bf16x3" run tlod_conv_wgrad_bs_f32 (split-bf16,
+    same slab reduction), "f32" the f32-input MFMA kernel."""
+    m = os.environ.get("TLOD_WGRAD_MATH") or conv_math()
+    if m not in MATHS:
+        raise ValueError(f"TLOD_WGRAD_MATH={m!r}: expected one of {MATHS}")
+    return m
+
+
+def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None):
     g = g.contiguous()
     x = x.contiguous()
     N, Cout, H, W = g.shape
@@ -167,6 +177,16 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False):
     L = _lib.lib()
     dw = out if out is not None else torch.empty((Cout, Cin, KS, KS), dtype=torch.float32,
                                                  device=g.device)
+    math = wgrad_math() if math is None else math
+    if _bs(KS, math):
+        nprod = 6 if math == "bf16x6" else 3
+        ws = _lib.workspace(L.tlod_conv_wgrad_bs_workspace_bytes(N, Cin, H, W, Cout, KS, nprod),
+                            g.device, "wgrad")
+        _timed("wgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
+            L.tlod_conv_wgrad_bs_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin,
+                                     H, W, Cout, KS, nprod, _lib.ptr(ws), ws.numel(),
+                                     _lib.stream_of(g)), "conv_wgrad_bs"), math)
+        return dw
     ws = _lib.workspace(L.tlod_conv_wgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "wgrad")
     _timed("wgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
         L.tlod_conv_wgrad_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin, H, W,
