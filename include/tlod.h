@@ -262,6 +262,20 @@ int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, int accum
                            int Cin, int H, int W, int Cout, int KS, int nprod, void* ws,
                            size_t ws_bytes, tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ Split-bf16 GEMM
+ * Replaces: the cuBLAS fp32 GEMMs of nn.Linear in RCNN_top (fc6/fc7, lib/DAF/vgg16.py:67-71
+ *   = torchvision vgg16().classifier[:-1]) and the DA instance head (lib/DAF/DA.py:53-73):
+ *   forward x W^T, input gradient dy W and weight gradient dy^T x.
+ * c[m][n] = sum_k A(m,k) B(n,k) (+ bias[n], may be NULL), c row-major M x N, contiguous.
+ * A(m,k) = a[m*K + k] if a_kcontig else a[k*M + m];  B(n,k) = b[n*K + k] if b_kcontig else
+ * b[k*N + n].  Operands split exactly into bf16 planes, nprod (6 or 3) products per f32
+ * product on the bf16 MFMA, f32 accumulation; split-K through a caller workspace of
+ * tlod_gemm_bs_workspace_bytes (fixed-order reduction: deterministic). */
+size_t tlod_gemm_bs_workspace_bytes(int M, int N, int K, int a_kcontig, int b_kcontig, int nprod);
+int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c, int M, int N,
+                     int K, int a_kcontig, int b_kcontig, int nprod, void* ws, size_t ws_bytes,
+                     tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ ResNet101 extras
  * Replaces: cuDNN for the ResNet101 stem conv1 7x7/2 + bn1 + relu (lib/DAF/resnet.py:107-110,
  *   frozen, forward only) and the stride-2 1x1 convolutions of the caffe-style bottleneck

@@ -1,0 +1,86 @@
+"""Split-bf16 GEMM (tlod_gemm_bs_f32) and tlod.linear.Linear vs a PyTorch fp64 CPU
+reference.
+
+Bars (normwise relative / elementwise vs max|ref|): bf16x6 1e-5 / 1e-4 — f32-level error
+(the three bf16 planes carry the f32 mantissa exactly, the dropped cross terms are below
+2^-24 relative); bf16x3 5e-5 / 5e-4.  Every operand layout (K- or M/N-contiguous), ragged
+M/N/K (tile edges, K tails inside a 16-deep chunk, odd strides for the unaligned loads),
+the split-K path and the head's real shapes (fc6 / fc7 with 556 RoIs).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+BARS = {"bf16x6": (1e-5, 1e-4), "bf16x3": (5e-5, 5e-4)}
+
+
+def _close(got, ref, math):
+    tol, etol = BARS[math]
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    nrm = float((got - ref).norm() / max(float(ref.norm()), 1e-30))
+    assert nrm <= tol, f"{math}: normwise rel err {nrm:.3e}"
+    assert float((got - ref).abs().max()) <= etol * float(ref.abs().max()) + 1e-30
+    return nrm
+
+
+@pytest.mark.parametrize("math", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("M,N,K", [(556, 300, 1000), (1, 7, 3), (37, 513, 17), (256, 256, 16),
+                                   (300, 1024, 4105), (5, 3000, 64)])
+def test_gemm_layouts(M, N, K, ak, bk, math):
+    from tlod.linear import gemm
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + 10 * ak + bk)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    a = A if ak else A.t().contiguous()
+    b = B if bk else B.t().contiguous()
+    c = gemm(a.to(dev), b.to(dev), M, N, K, ak, bk, bias.to(dev), math)
+    _close(c, A.double() @ B.double().t() + bias.double(), math)
+
+
+def test_gemm_split_k_deterministic():
+    """A deep-K / few-tile product takes the split-K slab path; results repeat bitwise."""
+    from tlod import _lib
+    from tlod.linear import gemm
+    M, N, K = 300, 512, 25088
+    assert _lib.lib().tlod_gemm_bs_workspace_bytes(M, N, K, 1, 1, 6) > 0
+    g = torch.Generator().manual_seed(1)
+    A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    c1 = gemm(A.to(dev), B.to(dev), M, N, K, 1, 1)
+    c2 = gemm(A.to(dev), B.to(dev), M, N, K, 1, 1)
+    assert torch.equal(c1, c2)
+    _close(c1, A.double() @ B.double().t(), "bf16x6")
+
+
+@pytest.mark.parametrize("R,I,O", [(556, 25088, 4096), (556, 4096, 4096), (556, 4096, 1024),
+                                   (256, 4105, 1024), (3, 100, 20)])
+def test_linear_fwd_bwd(R, I, O):
+    """tlod.linear.Linear forward, input / weight / bias gradients vs nn.Linear in fp64."""
+    from tlod.linear import Linear
+    torch.manual_seed(R + I + O)
+    lin = Linear(I, O)
+    ref = torch.nn.Linear(I, O).double()
+    ref.load_state_dict({k: v.double() for k, v in lin.state_dict().items()})
+    lin = lin.to(dev)
+    x = torch.randn(R, I)
+    gy = torch.randn(R, O)
+    xd = x.to(dev).requires_grad_(True)
+    y = lin(xd)
+    y.backward(gy.to(dev))
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(gy.double())
+    _close(y, yr, "bf16x6")
+    _close(xd.grad, xr.grad, "bf16x6")
+    _close(lin.weight.grad, ref.weight.grad, "bf16x6")
+    _close(lin.bias.grad, ref.bias.grad, "bf16x6")
+
+
+def test_linear_state_dict_matches_nn_linear():
+    from tlod.linear import Linear
+    a, b = Linear(25088, 4096), torch.nn.Linear(25088, 4096)
+    assert a.state_dict().keys() == b.state_dict().keys()
+    assert a.weight.shape == b.weight.shape and a.bias.shape == b.bias.shape

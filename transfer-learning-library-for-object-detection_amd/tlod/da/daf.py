@@ -20,6 +20,7 @@ import torch.nn.functional as F
 
 from ..config import cfg
 from ..conv import Conv2d
+from ..linear import Linear
 from ..detector.losses import smooth_l1_loss
 from ..detector.vgg16 import vgg16_base, vgg16_top
 from ..roi_align import RoIAlignAvg
@@ -84,10 +85,10 @@ class _InstanceDA(nn.Module):
 
     def __init__(self, in_dim=4096):
         super().__init__()
-        self.dc_ip1 = nn.Linear(in_dim, 1024)
+        self.dc_ip1 = Linear(in_dim, 1024)
         self.dc_relu1 = nn.ReLU()
         self.dc_drop1 = nn.Dropout(p=0.5)
-        self.dc_ip2 = nn.Linear(1024, 1024)
+        self.dc_ip2 = Linear(1024, 1024)
         self.dc_relu2 = nn.ReLU()
         self.dc_drop2 = nn.Dropout(p=0.5)
         self.clssifer = nn.Linear(1024, 1)

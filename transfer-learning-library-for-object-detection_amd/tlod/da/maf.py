@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from .. import _lib
 from ..conv import Conv2d
+from ..linear import Linear
 from .daf import _ImageDA, _fasterRCNN as _DAFBase, grad_reverse, image_label
 from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
@@ -122,9 +123,9 @@ class _InstanceDA_w(nn.Module):
 
     def __init__(self, input):
         super().__init__()
-        self.dc_ip1 = nn.Linear(input, 1024)
+        self.dc_ip1 = Linear(input, 1024)
         self.dc_relu1 = nn.ReLU()
-        self.dc_ip2 = nn.Linear(1024, 1024)
+        self.dc_ip2 = Linear(1024, 1024)
         self.dc_relu2 = nn.ReLU()
         self.clssifer = nn.Linear(1024, 2)
 

@@ -4,11 +4,13 @@
 ``RCNN_base.{0,2,5,...}.weight/bias`` as in the reference) with every conv+ReLU pair
 fused into one libtlod conv (the ReLU slots become nn.Identity).  Layers 0-9 (conv1_x,
 conv2_x) are frozen (vgg16.py:52-53).  ``RCNN_top`` = classifier[:-1]:
-Linear(25088,4096) ReLU Dropout Linear(4096,4096) ReLU Dropout (hipBLASLt GEMMs).
+Linear(25088,4096) ReLU Dropout Linear(4096,4096) ReLU Dropout (tlod.linear: split-bf16
+GEMMs in libtlod).
 """
 import torch.nn as nn
 
 from ..conv import Conv2d, vgg_init_
+from ..linear import Linear
 
 # split points (shared frozen prefix end, conv3 end, conv4 end) of RCNN_base for the MAF /
 # ATF taps: conv3 = features[:16], conv34 = [16:23], conv45 = [23:-1] (lib/MAF/vgg16.py:84-86)
@@ -36,7 +38,7 @@ def vgg16_base(frozen_layers=10):
 
 
 def vgg16_top():
-    fc6, fc7 = nn.Linear(512 * 7 * 7, 4096), nn.Linear(4096, 4096)
+    fc6, fc7 = Linear(512 * 7 * 7, 4096), Linear(4096, 4096)
     for m in (fc6, fc7):  # torchvision VGG Linear init
         m.weight.data.normal_(0, 0.01)
         m.bias.data.zero_()

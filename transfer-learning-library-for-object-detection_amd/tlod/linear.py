@@ -1,0 +1,83 @@
+"""Fully connected layers on libtlod's split-bf16 GEMM (tlod_gemm_bs_f32).
+
+``Linear`` is a drop-in for the ``nn.Linear`` modules of the detection head
+(RCNN_top = torchvision vgg16().classifier[:-1]: fc6 25088->4096, fc7 4096->4096,
+lib/DAF/vgg16.py:67-71) and of the DA instance discriminator (lib/DAF/DA.py:53-73): same
+parameters, same state_dict keys, same init.  Forward, input gradient and weight gradient
+each run as one GEMM in libtlod (operands split exactly into bf16 planes on the fly, f32
+accumulation: f32-level error, tests/test_linear_gpu.py); the bias gradient is a column
+sum.  Layers narrower than one 256-wide tile (the 9-way class / 36-way box heads, the
+1-way DA classifier) stay on nn.Linear, where a 256x256 tile would be mostly padding.
+"""
+import os
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+MATHS = ("bf16x6", "bf16x3")
+
+
+def linear_math():
+    """TLOD_LINEAR_MATH: "bf16x6" (default, f32-level error), "bf16x3" (~5e-6), or "f32"
+    (nn.Linear's GEMM library path, for A/B comparison)."""
+    m = os.environ.get("TLOD_LINEAR_MATH", "bf16x6")
+    if m not in MATHS + ("f32",):
+        raise ValueError(f"TLOD_LINEAR_MATH={m!r}")
+    return m
+
+
+def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6"):
+    """c[M][N] = sum_k A(m,k) B(n,k) (+ bias[n]) — see include/tlod.h tlod_gemm_bs_f32."""
+    _lib.require_cuda(a, b)
+    if a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise TypeError("tlod gemm computes in fp32 (the reference's dtype)")
+    a, b = a.contiguous(), b.contiguous()
+    nprod = 6 if math == "bf16x6" else 3
+    L = _lib.lib()
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    ws = _lib.workspace(L.tlod_gemm_bs_workspace_bytes(M, N, K, a_kcontig, b_kcontig, nprod),
+                        a.device, "gemm")
+    bias = bias.detach().contiguous() if bias is not None else None
+    _lib.check(L.tlod_gemm_bs_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K,
+                                  int(a_kcontig), int(b_kcontig), nprod, _lib.ptr(ws), ws.numel(),
+                                  _lib.stream_of(a)), "gemm_bs")
+    return c
+
+
+class LinearFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, math):
+        R, I = x.shape
+        O = weight.shape[0]
+        y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math)          # x W^T (+ b)
+        ctx.math = math
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        R, I = x.shape
+        O = weight.shape[0]
+        dy = dy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dy, weight.detach(), R, I, O, 1, 0, None, ctx.math)  # dy W
+        if ctx.needs_input_grad[1]:
+            dw = gemm(dy, x, O, I, R, 0, 0, None, ctx.math)                # dy^T x
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+        return dx, dw, db, None
+
+
+class Linear(nn.Linear):
+    """nn.Linear with the libtlod GEMM (2-D input [rows, in_features])."""
+
+    def forward(self, x):
+        m = linear_math()
+        if m == "f32" or x.dim() != 2:
+            return super().forward(x)
+        return LinearFunction.apply(x, self.weight, self.bias, m)
