@@ -9,6 +9,7 @@ out=../../build_variants/$name
 mkdir -p $out
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../../include $*"
 /opt/rocm/bin/hipcc $FLAGS -c conv.hip -o $out/conv.o
-objs=$(ls build/*.o | grep -v '/conv.o$')
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libtlod.so $out/conv.o $objs
+/opt/rocm/bin/hipcc $FLAGS -c gemm.hip -o $out/gemm.o
+objs=$(ls build/*.o | grep -v '/conv.o$' | grep -v '/gemm.o$')
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libtlod.so $out/conv.o $out/gemm.o $objs
 echo $out/libtlod.so

@@ -36,6 +36,12 @@ namespace tlod {
 #ifndef TLOD_CONV_SGB_W
 #define TLOD_CONV_SGB_W 0
 #endif
+// Split-bf16 kernels: store the next chunk's staged operands to the other LDS buffer in
+// the middle of the MFMA phase (the other wave of the SIMD keeps the MFMA pipe busy while
+// this one splits and writes) instead of after it.  0 = after the MFMA phase.
+#ifndef TLOD_MID_STORE
+#define TLOD_MID_STORE 1
+#endif
 #ifndef TLOD_CONV_OCC
 #define TLOD_CONV_OCC __attribute__((amdgpu_waves_per_eu(2, 4)))
 #endif
@@ -342,7 +348,14 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
 
 constexpr int kBsKP = 80;  // packed k per chunk: 10 taps (9 + zero pad) x 8 channels
 
-template <int WM, int WN, int MI, int NJ, int NP>
+// Band tiles (narrow maps, W <= ~100): a tile is 512 consecutive flattened pixels
+// p = h*W + w (16 groups of 32, one per MFMA column block) instead of 16 rows x 32 columns,
+// so a 37x75 map wastes 10% of the MFMA columns instead of 40%.  The staged input patch is
+// then full-width rows h0-1 .. h1+1 of the band, at most kBandPos positions.
+constexpr int kBandPos = 960;
+__host__ __device__ constexpr bool band_fits(int W) { return (511 / W + 4) * (W + 2) <= kBandPos; }
+
+template <int WM, int WN, int MI, int NJ, int NP, bool BAND = false>
 struct BsCfg {
   static constexpr int NPL = NP == 6 ? 3 : 2;   // bf16 planes used
   static constexpr int NT = WM * WN * 64;
@@ -353,18 +366,19 @@ struct BsCfg {
   static constexpr int STEPS = 5;               // tap pairs (0,1) (2,3) (4,5) (6,7) (8,pad)
   static constexpr int AROW = 176;              // bytes per weight row per plane (160 used)
   static constexpr int A_PLANE = BM * AROW;     // bytes
-  static constexpr int B_PLANE = PP * 16;       // bytes
+  static constexpr int BPOS = BAND ? kBandPos : PP;  // staged patch positions
+  static constexpr int B_PLANE = BPOS * 16;     // bytes
   static constexpr int BUF = NPL * (A_PLANE + B_PLANE);
   static constexpr int LDS_BYTES = 2 * BUF + 2 * BM * 4;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int WM, int WN, int MI, int NJ, int NP>
+template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
 __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
     const float* __restrict__ X, const unsigned short* __restrict__ Wp, Epi epi,
     float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int tiles_m, int tiles_w,
     int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab) {
-  using C = BsCfg<WM, WN, MI, NJ, NP>;
+  using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int n_tiles = tiles_m * tiles_w * tiles_h * N;
@@ -383,7 +397,16 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
   const int tw = t % tiles_w; t /= tiles_w;
   const int th = t % tiles_h; t /= tiles_h;
   const int n = t;
-  const int m0 = mt * C::BM, w0 = tw * C::TW, h0 = th * C::TH;
+  const int HWi = H * W;
+  // 2D tile: rows h0.., columns w0..; band tile: pixels p0 .. p0+511, patch rows from h0-1,
+  // patch width PW = W + 2 (row pitch of the staged positions)
+  const int m0 = mt * C::BM;
+  const int p0 = tw * C::TH * C::TW;
+  const int w0 = BAND ? 0 : tw * C::TW;
+  const int h0 = BAND ? p0 / W : th * C::TH;
+  const int PWr = BAND ? W + 2 : C::PW;
+  const int PPr = BAND ? (min(p0 + C::TH * C::TW, HWi) - 1) / W - h0 + 3 : C::PH;  // patch rows
+  const int npos = PPr * PWr;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -400,14 +423,27 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 #pragma unroll
   for (int st = 0; st < C::STEPS; ++st) {
     const int tap = min(2 * st + khalf, 8);
-    b_off[st] = C::NPL * C::A_PLANE + ((wn * NJ + tap / 3) * C::PW + l32 + tap % 3) * 16;
+    b_off[st] = C::NPL * C::A_PLANE + (BAND ? (tap / 3 - 1) * PWr + tap % 3 - 1
+                                            : (wn * NJ + tap / 3) * C::PW + l32 + tap % 3) * 16;
+  }
+  // band: this lane's pixel of column block j sits at patch position (h - h0 + 1, w + 1)
+  int b_pix[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (BAND) {
+      const int p = min(p0 + (wn * NJ + j) * 32 + l32, HWi - 1);
+      const int h = p / W;
+      b_pix[j] = ((h - h0 + 1) * PWr + p - h * W + 1) * 16;
+    } else {
+      b_pix[j] = j * C::PW * 16;
+    }
   }
 
   // ---- staging.  A: NPL planes x BM rows x 10 16-B segments; B: PP positions x 8 ch.
   constexpr int A_SEG = kBsKP / 8;                   // 16-B segments per row per chunk
   constexpr int A_N = C::NPL * C::BM * A_SEG;
   constexpr int A_IT = (A_N + C::NT - 1) / C::NT;
-  constexpr int B_IT = (C::PP + C::NT - 1) / C::NT;
+  constexpr int B_IT = (C::BPOS + C::NT - 1) / C::NT;
   int a_lds[A_IT];
   unsigned a_gl[A_IT];  // element offsets of the chunk-0 segment (planes < 2^31 elements)
   unsigned a_valid = 0;
@@ -423,15 +459,14 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
   }
   int b_pos[B_IT], b_goff[B_IT];
   unsigned b_pvalid = 0;
-  const int HWi = H * W;
 #pragma unroll
   for (int i = 0; i < B_IT; ++i) {
     const int pos = tid + i * C::NT;
-    const int r = pos / C::PW, c = pos % C::PW;
+    const int r = pos / PWr, c = pos % PWr;
     const int gh = h0 - 1 + r, gw = w0 - 1 + c;
-    const bool ok = pos < C::PP && gh >= 0 && gh < H && gw >= 0 && gw < W;
+    const bool ok = pos < npos && gh >= 0 && gh < H && gw >= 0 && gw < W;
     b_pvalid |= (unsigned)ok << i;
-    b_pos[i] = pos < C::PP ? C::NPL * C::A_PLANE + pos * 16 : -1;
+    b_pos[i] = pos < npos ? C::NPL * C::A_PLANE + pos * 16 : -1;
     b_goff[i] = ok ? gh * W + gw : 0;
   }
   u32x4 ra[A_IT];
@@ -504,6 +539,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
     if (more) load_chunk(ch + 1);
 #pragma unroll
     for (int st = 0; st < C::STEPS; ++st) {
+      if (TLOD_MID_STORE && more && st == C::STEPS / 2) store_chunk(smem + ((it + 1) & 1) * C::BUF);
       u32x4 a[MI][3], b[NJ][3];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -515,8 +551,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int pl = 0; pl < C::NPL; ++pl)
-          b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_off[st] + pl * C::B_PLANE +
-                                                     j * C::PW * 16);
+          b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_off[st] + pl * C::B_PLANE + b_pix[j]);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -531,7 +566,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
           acc[i][j] = mfma_bf16(a[i][0], b[j][0], acc[i][j]);
         }
     }
-    if (more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
+    if (!TLOD_MID_STORE && more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
     __syncthreads();
   }
 
@@ -559,13 +594,15 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int h = h0 + wn * NJ + j;
-      if (h >= H || w >= W) continue;
+      const int pband = p0 + (wn * NJ + j) * 32 + l32;
+      if (BAND ? pband >= HWi : (h >= H || w >= W)) continue;
+      const int pix = BAND ? pband : h * W + w;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
         const int co = m0 + ml;
         if (co < Cout) {
-          const size_t idx = ((size_t)co * H + h) * W + w;
+          const size_t idx = (size_t)co * HWi + pix;
           float v = acc[i][j][r];
           if (has_scale) v *= scale_s[ml];
           v += bias_s[ml];
@@ -993,6 +1030,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
         b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_rd + pl * C::B_PLANE + j * 32 * C::PITCH);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
+      if (TLOD_MID_STORE && more && i == MI / 2) store_chunk(smem + ((it + 1) & 1) * C::BUF);
       u32x4 a[3];
 #pragma unroll
       for (int pl = 0; pl < C::NPL; ++pl)
@@ -1009,7 +1047,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
         acc[i][j] = mfma_bf16(a[0], b[j][0], acc[i][j]);
       }
     }
-    if (more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
+    if (!TLOD_MID_STORE && more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
     __syncthreads();
   }
 
@@ -1049,7 +1087,7 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
 __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
     const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int th_rows,
     int tiles_m, int tiles_w, int tiles_h, Epi epi, int Cout, int H, int W,
-    float* __restrict__ Y) {
+    float* __restrict__ Y, int band) {
   const int tp = th_rows * 32, tile_elems = bm * tp;
   const int per_tile = (tile_elems + 1023) / 1024;
   const int ti = blockIdx.x / per_tile;
@@ -1063,11 +1101,19 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
   for (int e = (blockIdx.x % per_tile) * 1024 + threadIdx.x;
        e < min(tile_elems, (blockIdx.x % per_tile + 1) * 1024); e += 256) {
     const int ml = e / tp, pix = e % tp;
-    const int co = mt * bm + ml, h = th * th_rows + pix / 32, w = tw * 32 + pix % 32;
-    if (co >= Cout || h >= H || w >= W) continue;
+    const int co = mt * bm + ml;
+    int p;  // flattened pixel
+    if (band) {
+      p = tw * tp + pix;
+      if (co >= Cout || p >= H * W) continue;
+    } else {
+      const int h = th * th_rows + pix / 32, w = tw * 32 + pix % 32;
+      if (co >= Cout || h >= H || w >= W) continue;
+      p = h * W + w;
+    }
     float v = S[e];
     for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
-    const size_t idx = (((size_t)n * Cout + co) * H + h) * W + w;
+    const size_t idx = ((size_t)n * Cout + co) * (size_t)(H * W) + p;
     if (epi.scale) v *= epi.scale[co];
     if (epi.bias) v += epi.bias[co];
     if (epi.residual) v += epi.residual[idx];
@@ -1259,7 +1305,7 @@ static int launch_fwd(const float* X, const float* Wk, Epi epi, float* Y, int N,
     const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
     hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
                        p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
-                       p.tiles_h, epi, Cout, H, W, Y);
+                       p.tiles_h, epi, Cout, H, W, Y, 0);
     TLOD_LAUNCH_CHECK();
   }
   return kOk;
@@ -1304,24 +1350,35 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, Epi epi, float* Y,
 }
 
 // ---- split-bf16 forward launch (KS = 3)
-template <int WM, int WN, int MI, int NJ, int NP>
+// Band tiles pay off where 32-wide column tiles pad the map badly (conv5 / RPN at 37x75:
+// 40% padding; 75x150: 6%), and fit the staged patch only for narrow maps.
+static bool use_band(int H, int W) {
+  if (!band_fits(W) || tune_knob("TLOD_CONV_BAND", 1) == 0) return false;
+  const double util2d = (double)H * W / ((double)div_up(H, 16) * 16 * div_up(W, 32) * 32);
+  const double utilb = (double)H * W / ((double)div_up(H * W, 512) * 512);
+  return utilb > util2d * 1.05;
+}
+
+template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
 static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout) {
-  using C = BsCfg<WM, WN, MI, NJ, NP>;
-  static const int slots = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP>, C::NT,
+  using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
+  static const int slots = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>, C::NT,
                                           C::LDS_BYTES);
   const int nchunks = div_up(Cin, C::CK);
   // cost model in f32-MFMA-equivalent time: the split products run ~16/NP x faster
-  return plan_schedule(div_up(Cout, C::BM), div_up(W, C::TW), div_up(H, C::TH), N, nchunks,
+  const int tw = BAND ? div_up(H * W, C::TH * C::TW) : div_up(W, C::TW);
+  const int th = BAND ? 1 : div_up(H, C::TH);
+  return plan_schedule(div_up(Cout, C::BM), tw, th, N, nchunks,
                        2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
                        C::BM * C::TH * C::TW, slots);
 }
 
-template <int WM, int WN, int MI, int NJ, int NP>
+template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
 static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, float* Y, int N,
                          int Cin, int H, int W, int Cout, float* slab, size_t slab_bytes,
                          hipStream_t s) {
-  using C = BsCfg<WM, WN, MI, NJ, NP>;
-  const FwdPlan p = plan_fwd_bs<WM, WN, MI, NJ, NP>(N, Cin, H, W, Cout);
+  using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
+  const FwdPlan p = plan_fwd_bs<WM, WN, MI, NJ, NP, BAND>(N, Cin, H, W, Cout);
   const long long nwg = (long long)p.dp_tiles + (long long)p.n_tail() * (p.ksplit > 1 ? p.ksplit : 0);
   TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
   if (p.ksplit > 1 && slab_bytes < p.slab_bytes(C::BM, C::TH)) {
@@ -1329,7 +1386,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
     return kWorkspace;
   }
   const size_t lds = C::LDS_BYTES;
-  auto kern = conv_fwd_bs_kernel<WM, WN, MI, NJ, NP>;
+  auto kern = conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>;
   static bool attr = false;
   if (!attr) {
     TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1342,7 +1399,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
     const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
     hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
                        p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
-                       p.tiles_h, epi, Cout, H, W, Y);
+                       p.tiles_h, epi, Cout, H, W, Y, BAND ? 1 : 0);
     TLOD_LAUNCH_CHECK();
   }
   return kOk;
@@ -1359,17 +1416,22 @@ static int conv_fwd_bs_dispatch(const float* X, const unsigned short* Wp, Epi ep
     set_error("conv_bs: nprod must be 3 or 6");
     return kInvalidArg;
   }
-#define TLOD_BS_CFG(WM_, WN_, MI_, NJ_, NP_)                                                    \
+#define TLOD_BS_CFG(WM_, WN_, MI_, NJ_, NP_, BAND_)                                             \
   do {                                                                                          \
     if (ws_query) {                                                                             \
-      using C_ = BsCfg<WM_, WN_, MI_, NJ_, NP_>;                                                \
-      *ws_query = plan_fwd_bs<WM_, WN_, MI_, NJ_, NP_>(N, Cin, H, W, Cout).slab_bytes(C_::BM, C_::TH); \
+      using C_ = BsCfg<WM_, WN_, MI_, NJ_, NP_, BAND_>;                                         \
+      *ws_query = plan_fwd_bs<WM_, WN_, MI_, NJ_, NP_, BAND_>(N, Cin, H, W, Cout)               \
+                      .slab_bytes(C_::BM, C_::TH);                                              \
       return kOk;                                                                               \
     }                                                                                           \
-    return launch_fwd_bs<WM_, WN_, MI_, NJ_, NP_>(X, Wp, epi, Y, N, Cin, H, W, Cout, slab, sb, s); \
+    return launch_fwd_bs<WM_, WN_, MI_, NJ_, NP_, BAND_>(X, Wp, epi, Y, N, Cin, H, W, Cout,     \
+                                                         slab, sb, s);                          \
   } while (0)
-  if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6);
-  TLOD_BS_CFG(1, 8, 2, 2, 3);
+  const bool band = use_band(H, W);
+  if (nprod == 6 && band) TLOD_BS_CFG(1, 8, 2, 2, 6, true);
+  if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6, false);
+  if (band) TLOD_BS_CFG(1, 8, 2, 2, 3, true);
+  TLOD_BS_CFG(1, 8, 2, 2, 3, false);
 #undef TLOD_BS_CFG
 }
 

@@ -30,6 +30,10 @@ namespace tlod {
 
 namespace {
 
+#ifndef TLOD_MID_STORE
+#define TLOD_MID_STORE 1  // stage the next chunk mid-MFMA-phase (see conv.hip)
+#endif
+
 constexpr int kBN = 256, kTK = 16, kNT = 512;
 constexpr int kWM = 2, kWN = 4, kNJ = 2;  // M tile 64*MI (MI = 4 or 3), N tile 256
 constexpr int kPitchK = 48;    // [row][16 k] images
@@ -187,6 +191,7 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
         b[j][pl] = read_operand<BK>(buf + NPL * A_PL + pl * B_PL, wn * kNJ * 32 + j * 32, lane);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
+      if (TLOD_MID_STORE && more && i == MI / 2) store(smem + ((it + 1) & 1) * BUF);
       u32x4 a[3];
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl)
@@ -203,7 +208,7 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
         acc[i][j] = mfma_bf16(a[0], b[j][0], acc[i][j]);
       }
     }
-    if (more) store(smem + ((it + 1) & 1) * BUF);
+    if (!TLOD_MID_STORE && more) store(smem + ((it + 1) & 1) * BUF);
     __syncthreads();
   }
 
