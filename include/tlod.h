@@ -276,6 +276,19 @@ int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c
                      int K, int a_kcontig, int b_kcontig, int nprod, void* ws, size_t ws_bytes,
                      tlod_stream_t stream);
 
+/* Split-bf16 3x3 convolution as an implicit GEMM over (c, tap) x flattened pixels, for
+ * wide outputs (Cout >= 256): the forward of tlod_conv_fwd_ex_f32 (w_layout = 0: w is the
+ * nn.Conv2d weight [Cout][Cin][3][3] as is) or the dgrad (w_layout = 1: w is
+ * tlod_conv_pack_dgrad_f32's [(co*9 + s)][ci] pack, x = dy, Cin := the layer's Cout,
+ * Cout := the layer's Cin).  y = act(conv * scale + bias + residual), every epilogue
+ * pointer optional.  Workspace: tlod_conv3x3_gemm_bs_workspace_bytes (split-K slabs). */
+size_t tlod_conv3x3_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
+                                            int w_layout, int nprod);
+int tlod_conv3x3_gemm_bs_f32(const float* x, const float* w, int w_layout, const float* scale,
+                             const float* bias, const float* residual, float* y, int N, int Cin,
+                             int H, int W, int Cout, int relu, int nprod, void* ws,
+                             size_t ws_bytes, tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ ResNet101 extras
  * Replaces: cuDNN for the ResNet101 stem conv1 7x7/2 + bn1 + relu (lib/DAF/resnet.py:107-110,
  *   frozen, forward only) and the stride-2 1x1 convolutions of the caffe-style bottleneck

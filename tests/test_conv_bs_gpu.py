@@ -46,6 +46,50 @@ def test_conv_bs_fwd_dgrad(math, N, Cin, Cout, H, W):
     _close(dx, torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=1), math)
 
 
+GEMM_SHAPES = [  # N, Cin, Cout, H, W: >= 256 output channels (fwd) / input channels (dgrad)
+    (2, 256, 256, 30, 40), (1, 64, 300, 9, 33), (3, 257, 256, 5, 7), (1, 256, 260, 3, 3),
+    (1, 300, 512, 16, 16), (2, 512, 256, 37, 75), (1, 128, 256, 1, 40), (1, 16, 256, 40, 2),
+]
+
+
+@pytest.mark.parametrize("math", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("N,Cin,Cout,H,W", GEMM_SHAPES)
+def test_conv_gemm_fwd_dgrad(math, N, Cin, Cout, H, W):
+    """tlod_conv3x3_gemm_bs_f32 (im2col rows gathered per 16-deep k chunk, 256x256 tiles,
+    split-K slabs on small maps): forward with the full epilogue and dgrad through the
+    transposed pack; ragged K = Cin*9, maps narrower than a 4-pixel vector, image 0's first
+    rows (the per-dword load path)."""
+    from tlod.conv import _conv_gemm, pack_dgrad
+    g = torch.Generator().manual_seed(N * 100 + Cin + Cout + H + W)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    sc = torch.rand(Cout, generator=g) + 0.5
+    r = torch.randn(N, Cout, H, W, generator=g)
+    y = _conv_gemm(x.to(dev), w.to(dev), 0, b.to(dev), True, sc.to(dev), r.to(dev), Cout, math, "fwd")
+    ref = torch.relu(F.conv2d(x.double(), w.double(), padding=1) * sc.double().view(1, -1, 1, 1)
+                     + b.double().view(1, -1, 1, 1) + r.double())
+    _close(y * (ref > 0).to(dev), ref, math)  # mask flips at f32 rounding of 0 do not count
+    y0 = _conv_gemm(x.to(dev), w.to(dev), 0, None, False, None, None, Cout, math, "fwd")
+    _close(y0, F.conv2d(x.double(), w.double(), padding=1), math)
+    if Cin >= 256:
+        gy = torch.randn(N, Cout, H, W, generator=g)
+        dx = _conv_gemm(gy.to(dev), pack_dgrad(w.to(dev)), 1, None, False, None, None, Cin, math,
+                        "dgrad")
+        _close(dx, torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=1), math)
+
+
+def test_conv_gemm_matches_patch_kernel():
+    """The implicit-GEMM path and the patch-staged split-bf16 kernel agree to f32 rounding."""
+    from tlod.conv import _conv_bs, _conv_gemm, pack_bs
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 256, 40, 60, generator=g).to(dev)
+    w = (torch.randn(256, 256, 3, 3, generator=g) * 0.03).to(dev)
+    a = _conv_gemm(x, w, 0, None, False, None, None, 256, "bf16x6", "fwd")
+    b = _conv_bs(x, pack_bs(w, False), None, False, None, None, 256, 3, "bf16x6", "fwd")
+    assert float((a - b).norm() / b.norm()) < 1e-6
+
+
 WGRAD_SHAPES = SHAPES + [  # + maps narrower than an 8-pixel segment, single rows/columns
     (2, 32, 64, 5, 7), (1, 16, 32, 1, 40), (1, 16, 32, 40, 1), (3, 8, 36, 3, 3),
     (2, 512, 512, 37, 75),

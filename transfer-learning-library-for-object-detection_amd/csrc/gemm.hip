@@ -128,36 +128,17 @@ __device__ __forceinline__ u32x4 read_operand(const unsigned char* img, int base
   return u32x4{lo.x, lo.y, hi.x, hi.y};
 }
 
-template <int AK, int BK, int NP, int MI>
-__global__ void __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(2, 2)))
-gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
-               const float* __restrict__ bias, float* __restrict__ C, int M, int N, int K,
-               int tiles_m, int tiles_n, int splits, int chunks_per_split) {
+// The K loop shared by the GEMM and the implicit-GEMM convolution: double-buffered LDS
+// images of the two operands, the next chunk loaded to registers during the MFMAs and
+// split + stored to the other buffer half way through them.
+template <int AK, int BK, int NP, int MI, class SA, class SB>
+__device__ __forceinline__ void mainloop(SA& sa, SB& sb, f32x16 (&acc)[MI][kNJ], int c_begin,
+                                         int c_end, unsigned char* smem, int Ra, int Rb) {
   constexpr int NPL = NP == 6 ? 3 : 2;
   constexpr int A_PL = Img<AK>::PLANE, B_PL = Img<BK>::PLANE;
   constexpr int BUF = NPL * (A_PL + B_PL);
-  constexpr int BM = kWM * MI * 32;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-  const int nwg = tiles_m * tiles_n * splits;
-  int t = xcd_remap(blockIdx.x, nwg);
-  const int mt = t % tiles_m; t /= tiles_m;
-  const int nt = t % tiles_n;
-  const int split = t / tiles_n;
-  const int m0 = mt * BM, n0 = nt * kBN;
-  const int nchunks = (K + kTK - 1) / kTK;
-  const int c_begin = split * chunks_per_split;
-  const int c_end = min(nchunks, c_begin + chunks_per_split);
-
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / kWN, wn = wid % kWN;
-
-  Stager<AK, NPL, BM> sa;
-  Stager<BK, NPL, kBN> sb;
-  sa.init(A, M, K, m0, tid);
-  sb.init(B, N, K, n0, tid);
-
-  f32x16 acc[MI][kNJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -170,8 +151,8 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
     sb.store(buf + NPL * A_PL);
   };
   if (c_begin < c_end) {
-    sa.load(c_begin * kTK, M);
-    sb.load(c_begin * kTK, N);
+    sa.load(c_begin * kTK, Ra);
+    sb.load(c_begin * kTK, Rb);
     store(smem);
   }
   __syncthreads();
@@ -180,8 +161,8 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
     const unsigned char* buf = smem + (it & 1) * BUF;
     const bool more = c + 1 < c_end;
     if (more) {
-      sa.load((c + 1) * kTK, M);
-      sb.load((c + 1) * kTK, N);
+      sa.load((c + 1) * kTK, Ra);
+      sb.load((c + 1) * kTK, Rb);
     }
     u32x4 b[kNJ][3];
 #pragma unroll
@@ -211,36 +192,88 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
     if (!TLOD_MID_STORE && more) store(smem + ((it + 1) & 1) * BUF);
     __syncthreads();
   }
+}
 
-  // splits == 1: C (+ bias); else slab[split][M][N] (bias added by the reduce)
-  float* out = splits == 1 ? C : C + (size_t)split * M * N;
-  const bool add_bias = splits == 1 && bias != nullptr;
+template <int AK, int BK, int NP, int MI>
+__global__ void __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
+               const float* __restrict__ bias, float* __restrict__ C, float* __restrict__ slab,
+               int M, int N, int K, int tiles_m, int tiles_n, int dp_tiles, int ksplit,
+               int chunks_per_split) {
+  constexpr int NPL = NP == 6 ? 3 : 2;
+  constexpr int BM = kWM * MI * 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  // whole tiles first, then the tail tiles split over K (plan_tail)
+  const int n_tail = tiles_m * tiles_n - dp_tiles;
+  const bool direct = (int)blockIdx.x < dp_tiles;
+  int t, split = 0, ti = 0;
+  if (direct) {
+    t = xcd_remap(blockIdx.x, dp_tiles);
+  } else {
+    const int u = xcd_remap(blockIdx.x - dp_tiles, n_tail * ksplit);
+    ti = u % n_tail;
+    split = u / n_tail;
+    t = dp_tiles + ti;
+  }
+  const int mt = t % tiles_m;
+  const int nt = t / tiles_m;
+  const int m0 = mt * BM, n0 = nt * kBN;
+  const int nchunks = (K + kTK - 1) / kTK;
+  const int c_begin = direct ? 0 : split * chunks_per_split;
+  const int c_end = direct ? nchunks : min(nchunks, c_begin + chunks_per_split);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / kWN, wn = wid % kWN;
+
+  Stager<AK, NPL, BM> sa;
+  Stager<BK, NPL, kBN> sb;
+  sa.init(A, M, K, m0, tid);
+  sb.init(B, N, K, n0, tid);
+  f32x16 acc[MI][kNJ];
+  mainloop<AK, BK, NP, MI>(sa, sb, acc, c_begin, c_end, smem, M, N);
+
+  // direct tiles: C (+ bias); tail pieces: tile-local slab (bias added by the reduce)
+  float* St = slab + ((size_t)split * n_tail + ti) * BM * kBN;
   const int l32 = lane & 31, khalf = lane >> 5;
 #pragma unroll
   for (int j = 0; j < kNJ; ++j) {
-    const int n = n0 + wn * kNJ * 32 + j * 32 + l32;
-    if (n >= N) continue;
-    const float bv = add_bias ? bias[n] : 0.f;
+    const int nl = wn * kNJ * 32 + j * 32 + l32;
+    const int n = n0 + nl;
+    const float bv = direct && bias != nullptr && n < N ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-        if (m < M) out[(size_t)m * N + n] = acc[i][j][r] + bv;
+        const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int m = m0 + ml;
+        if (!direct)
+          St[ml * kBN + nl] = acc[i][j][r];
+        else if (m < M && n < N)
+          C[(size_t)m * N + n] = acc[i][j][r] + bv;
       }
   }
 }
 
-// C[m][n] = sum_s slab[s][m][n] (+ bias[n]), fixed split order.
-__global__ void gemm_slab_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N,
-                                        const float* __restrict__ bias, float* __restrict__ C) {
-  const size_t count = (size_t)M * N;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
-       i += (size_t)gridDim.x * blockDim.x) {
-    float s = slab[i];
-    for (int k = 1; k < splits; ++k) s += slab[(size_t)k * count + i];
-    if (bias) s += bias[i % N];
-    C[i] = s;
+// Tail tiles: C[m][n] = sum_s slab[s][tile][m][n] (+ bias[n]), fixed split order.  One
+// workgroup per (tail tile, 1024 elements).
+__global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
+    const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tiles_m,
+    int M, int N, const float* __restrict__ bias, float* __restrict__ C) {
+  const int tile_elems = bm * kBN;
+  const int per_tile = tile_elems / 1024;
+  const int ti = blockIdx.x / per_tile;
+  const int t = dp_tiles + ti;
+  const int mt = t % tiles_m, nt = t / tiles_m;
+  const size_t stride = (size_t)n_tail * tile_elems;
+  const float* S = slab + (size_t)ti * tile_elems;
+  const int e0 = (blockIdx.x % per_tile) * 1024;
+  for (int e = e0 + threadIdx.x; e < e0 + 1024; e += 256) {
+    const int m = mt * bm + e / kBN, n = nt * kBN + e % kBN;
+    if (m >= M || n >= N) continue;
+    float v = S[e];
+    for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
+    C[(size_t)m * N + n] = v + (bias ? bias[n] : 0.f);
   }
 }
 
@@ -260,22 +293,33 @@ int slots_of(K kern, size_t lds) {
   return cached = per_cu * cus;
 }
 
-// Split count: fill whole rounds of the resident slots, >= 8 chunks per piece, and do not
-// let the slab round trip (2 sp + 1 passes over M*N floats) outweigh the compute saved.
-int pick_gemm_splits(int tiles, int nchunks, int slots, double chunk_s, double mn_bytes) {
-  int best = 1;
-  double best_t = 1e30;
-  for (int sp = 1; sp <= std::max(1, std::min(64, nchunks / 8)); ++sp) {
-    const int cps = div_up(nchunks, sp);
-    const int esp = div_up(nchunks, cps);
-    const long long rounds = ((long long)tiles * esp + slots - 1) / slots;
-    const double t = (double)rounds * cps * chunk_s + (esp > 1 ? (2.0 * esp + 1.0) * mn_bytes / 4e12 : 0.0);
-    if (t < best_t * 0.999) {
-      best_t = t;
-      best = esp;
+struct TailPlan {
+  int dp_tiles, ksplit, cps;
+};
+
+// Whole rounds of tiles over the full K, the last partial round split over K when that
+// beats running it as a mostly idle round (cost model: tile time at the slot rate, the
+// slab round trip at 4 TB/s, 6 us per reduce launch).
+TailPlan plan_tail(int T, int nchunks, int slots, double tile_s, double tile_bytes) {
+  TailPlan p{T, 1, nchunks};
+  double best = (double)((T + slots - 1) / slots) * tile_s;
+  const int q = T / slots;
+  for (int k = 2; k <= std::min(16, nchunks / 2); ++k) {
+    const int cps = div_up(nchunks, k);
+    const int kk = div_up(nchunks, cps);
+    for (int dp : {q * slots, 0}) {
+      const int tail = T - dp;
+      if (tail <= 0) continue;
+      const double t = (double)dp / slots * tile_s +
+                       (double)(((long long)tail * kk + slots - 1) / slots) * tile_s * cps / nchunks +
+                       (2.0 * kk + 1.0) * tail * tile_bytes / 4e12 + 6e-6;
+      if (t < best * 0.97) {
+        best = t;
+        p = TailPlan{dp, kk, cps};
+      }
     }
   }
-  return best;
+  return p;
 }
 
 template <int AK, int BK, int NP, int MI>
@@ -283,34 +327,41 @@ struct Gemm {
   static constexpr int NPL = NP == 6 ? 3 : 2;
   static constexpr int kBM = kWM * MI * 32;
   static constexpr size_t kLds = 2 * NPL * (Img<AK>::PLANE + Img<BK>::PLANE);
-  static int splits(int M, int N, int K) {
+  static TailPlan plan(int M, int N, int K) {
     const int slots = slots_of(gemm_bs_kernel<AK, BK, NP, MI>, kLds);
     const int tiles = div_up(M, kBM) * div_up(N, kBN);
-    const double chunk_s = 2.0 * kBM * kBN * kTK * NP / (2516.6e12 * 0.5 / slots);
-    return pick_gemm_splits(tiles, div_up(K, kTK), slots, chunk_s, 4.0 * M * N);
+    const int nchunks = div_up(K, kTK);
+    // bf16 MFMA time of one whole tile per resident slot at ~50% of the dense peak
+    const double tile_s = 2.0 * kBM * kBN * kTK * NP * nchunks / (2516.6e12 * 0.5 / slots);
+    return plan_tail(tiles, nchunks, slots, tile_s, 4.0 * kBM * kBN);
+  }
+  static size_t ws_bytes(int M, int N, int K) {
+    const TailPlan p = plan(M, N, K);
+    const int tiles = div_up(M, kBM) * div_up(N, kBN);
+    return p.ksplit > 1 ? (size_t)p.ksplit * (tiles - p.dp_tiles) * kBM * kBN * sizeof(float) : 0;
   }
   static int run(const float* A, const float* B, const float* bias, float* C, int M, int N, int K,
-                 float* ws, size_t ws_bytes, hipStream_t s) {
-    const int sp = splits(M, N, K);
-    if (sp > 1 && ws_bytes < (size_t)sp * M * N * sizeof(float)) {
+                 float* ws, size_t ws_bytes_, hipStream_t s) {
+    const TailPlan p = plan(M, N, K);
+    if (ws_bytes_ < ws_bytes(M, N, K)) {
       set_error("tlod_gemm_bs_f32: workspace too small");
       return kWorkspace;
     }
     const int tiles_m = div_up(M, kBM), tiles_n = div_up(N, kBN);
-    const int cps = div_up(div_up(K, kTK), sp);
+    const int n_tail = tiles_m * tiles_n - p.dp_tiles;
     auto kern = gemm_bs_kernel<AK, BK, NP, MI>;
     static bool attr = false;
     if (!attr) {
       TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
       attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3(tiles_m * tiles_n * sp), dim3(kNT), kLds, s, A, B, bias,
-                       sp > 1 ? ws : C, M, N, K, tiles_m, tiles_n, sp, cps);
+    const int nwg = p.dp_tiles + (p.ksplit > 1 ? n_tail * p.ksplit : 0);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, A, B, bias, C, ws, M, N, K, tiles_m,
+                       tiles_n, p.dp_tiles, p.ksplit, p.cps);
     TLOD_LAUNCH_CHECK();
-    if (sp > 1) {
-      const size_t count = (size_t)M * N;
-      hipLaunchKernelGGL(gemm_slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count + 255) / 256, 4096)),
-                         dim3(256), 0, s, ws, sp, M, N, bias, C);
+    if (p.ksplit > 1) {
+      hipLaunchKernelGGL(gemm_tail_reduce_kernel, dim3(n_tail * (kBM * kBN / 1024)), dim3(256), 0,
+                         s, ws, p.ksplit, n_tail, p.dp_tiles, kBM, tiles_m, M, N, bias, C);
       TLOD_LAUNCH_CHECK();
     }
     return kOk;
@@ -318,7 +369,7 @@ struct Gemm {
 };
 
 template <typename F>
-int with_gemm(int M, int ak, int bk, int nprod, F&& f) {
+auto with_gemm(int M, int ak, int bk, int nprod, F&& f) {
   // M tile 192 when it pads M less (the 556 RoI rows of the head: 576 vs 768)
   const bool m192 = div_up(M, 192) * 192 < div_up(M, 256) * 256;
 #define TLOD_GEMM_CASE(A_, B_)                                                 \
@@ -329,9 +380,257 @@ int with_gemm(int M, int ak, int bk, int nprod, F&& f) {
   TLOD_GEMM_CASE(1, 1)
   TLOD_GEMM_CASE(1, 0)
   TLOD_GEMM_CASE(0, 0)
-  TLOD_GEMM_CASE(0, 1)
 #undef TLOD_GEMM_CASE
-  return kUnsupported;
+  // (0, 1): the callers pass 0/1 flags, so the four cases are exhaustive
+  if (m192) return nprod == 6 ? f(Gemm<0, 1, 6, 3>{}) : f(Gemm<0, 1, 3, 3>{});
+  return nprod == 6 ? f(Gemm<0, 1, 6, 4>{}) : f(Gemm<0, 1, 3, 4>{});
+}
+
+// ---------------------------------------------------------------- 3x3 conv as GEMM
+// Implicit GEMM for the stride-1 "same" 3x3 convolution with >= 256 output channels:
+//   Y[img][m][p] = act(scale[m] * sum_k A(m,k) B(p,k) + bias[m] + residual[img][m][p])
+// K = C*9 over (c, tap), B(p, (c,tap)) = X[img][c][p + (tap/3-1)*W + tap%3-1] when the tap
+// lies inside the map, else 0 (the im2col row, gathered straight from NCHW with one
+// buffer_load_dwordx4 per 4 pixels and a bit-range in-map mask; staged [16 k][256 px] and
+// read transposed like the GEMM's N-contiguous operand).  A = the weights as
+// [Cout][C*9] (forward: nn.Conv2d's own layout, AK = 1) or tlod_conv_pack_dgrad_f32's
+// [(co, tap)][ci] (dgrad: the transposed, flipped kernel, AK = 0).
+struct ConvEpi {
+  const float* scale;
+  const float* bias;
+  const float* residual;
+  int relu;
+};
+
+template <int NPL>
+struct Im2colStager {
+  static constexpr int IT = 2;  // 16 k rows x 256 pixels / 512 lanes / 4
+  i32x4 rsrc;
+  int xoff, kr, p, c4, h0, w0, C, H, W, P, K;
+  bool neg_risk;
+  unsigned tmask;
+  f32x4v r[IT];
+  unsigned mask[IT];
+
+  __device__ void init(const float* X, int N, int C_, int H_, int W_, int img, int p0, int tid) {
+    C = C_; H = H_; W = W_; P = H * W; K = C * 9;
+    rsrc = make_buffer_rsrc(X, (unsigned)N * (unsigned)C * (unsigned)P * 4u);
+    xoff = img * C * P;
+    kr = tid >> 6;
+    c4 = (tid & 63) * 4;
+    p = p0 + c4;
+    const int pc = min(p, P - 1);
+    h0 = pc / W;
+    w0 = pc - h0 * W;
+    tmask = lt_mask4(P - p);
+    // a tap vector can start before the tensor only in image 0's first row band
+    neg_risk = img == 0 && p0 <= W;
+  }
+  __device__ void load(int kc, int) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int k = kc + kr + 8 * i;
+      const int c = k / 9, t = k - 9 * c;
+      const int dh = t / 3 - 1, dw = t - 3 * (t / 3) - 1;
+      const int o = xoff + c * P + dh * W + dw + p;
+      unsigned m;
+      if (W >= 4) {  // (h0, w0 + e) for e < ew, then (h0 + 1, e - ew): one wrap at most
+        const int ew = W - w0;
+        const bool r0 = (unsigned)(h0 + dh) < (unsigned)H;
+        const bool r1 = (unsigned)(h0 + 1 + dh) < (unsigned)H;
+        const unsigned m0v = lt_mask4(ew - max(dw, 0)) & ~lt_mask4(-w0 - dw);
+        const unsigned m1v = 0xfu & ~lt_mask4(ew + max(-dw, 0));
+        m = (r0 ? m0v : 0u) | (r1 ? m1v : 0u);
+      } else {
+        m = 0;
+        int h = h0, w = w0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          m |= (unsigned)((unsigned)(h + dh) < (unsigned)H && (unsigned)(w + dw) < (unsigned)W) << e;
+          if (++w == W) { w = 0; ++h; }
+        }
+      }
+      mask[i] = k < K ? m & tmask : 0u;
+      if (neg_risk && kc < 9) {
+        // per-dword: negative element offsets read out of range (0); the select keeps the
+        // backend from merging the four loads into one dwordx4 at the negative start
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          r[i][e] = raw_buffer_load_f32(rsrc, o + e >= 0 ? (o + e) * 4 : kBufOOB, 0, 0);
+      } else {
+        r[i] = raw_buffer_load_v4f32(rsrc, k < K ? o * 4 : kBufOOB, 0, 0);
+      }
+    }
+  }
+  __device__ void store(unsigned char* img) const {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ((mask[i] >> e) & 1) ? r[i][e] : 0.f;
+      unsigned sp[3][2];
+      split4<NPL>(v, sp);
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl)
+        *reinterpret_cast<uint2*>(img + pl * Img<0>::PLANE + (kr + 8 * i) * kPitchMN + 2 * c4) =
+            make_uint2(sp[pl][0], sp[pl][1]);
+    }
+  }
+};
+
+// Schedule: the first dp_tiles tiles (whole rounds of the resident slots) run over the full
+// K; the remaining tail tiles, which would leave most of the chip idle in a last partial
+// round, are split over K into ksplit pieces written to fixed slabs and reduced in order.
+template <int AK, int NP, int MI>
+__global__ void __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, ConvEpi epi,
+                    float* __restrict__ Y, float* __restrict__ slab, int N, int C, int H, int W,
+                    int Cout, int tiles_m, int tiles_n, int dp_tiles, int ksplit,
+                    int chunks_per_split) {
+  constexpr int NPL = NP == 6 ? 3 : 2;
+  constexpr int BM = kWM * MI * 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int P = H * W, K = C * 9;
+  const int n_tiles = tiles_m * tiles_n * N;
+  const int n_tail = n_tiles - dp_tiles;
+  const bool direct = (int)blockIdx.x < dp_tiles;
+  int t, split = 0, ti = 0;
+  if (direct) {
+    t = xcd_remap(blockIdx.x, dp_tiles);
+  } else {
+    const int u = xcd_remap(blockIdx.x - dp_tiles, n_tail * ksplit);
+    ti = u % n_tail;
+    split = u / n_tail;
+    t = dp_tiles + ti;
+  }
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int nt = t % tiles_n; t /= tiles_n;
+  const int img = t;
+  const int m0 = mt * BM, p0 = nt * kBN;
+  const int nchunks = (K + kTK - 1) / kTK;
+  const int c_begin = direct ? 0 : split * chunks_per_split;
+  const int c_end = direct ? nchunks : min(nchunks, c_begin + chunks_per_split);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / kWN, wn = wid % kWN;
+
+  Stager<AK, NPL, BM> sa;
+  sa.init(Wt, Cout, K, m0, tid);
+  Im2colStager<NPL> sb;
+  sb.init(X, N, C, H, W, img, p0, tid);
+  f32x16 acc[MI][kNJ];
+  mainloop<AK, 0, NP, MI>(sa, sb, acc, c_begin, c_end, smem, Cout, 0);
+
+  const int l32 = lane & 31, khalf = lane >> 5;
+  const size_t ybase = (size_t)img * Cout * P;
+  float* St = slab + ((size_t)split * n_tail + ti) * BM * kBN;
+#pragma unroll
+  for (int j = 0; j < kNJ; ++j) {
+    const int nl = wn * kNJ * 32 + j * 32 + l32;
+    const int pix = p0 + nl;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        const int co = m0 + ml;
+        float v = acc[i][j][r];
+        if (!direct) {  // tile-local slab, reduced by conv_tail_reduce_kernel
+          St[ml * kBN + nl] = v;
+          continue;
+        }
+        if (pix >= P || co >= Cout) continue;
+        const size_t idx = ybase + (size_t)co * P + pix;
+        if (epi.scale) v *= epi.scale[co];
+        if (epi.bias) v += epi.bias[co];
+        if (epi.residual) v += epi.residual[idx];
+        if (epi.relu) v = fmaxf(v, 0.f);
+        Y[idx] = v;
+      }
+  }
+}
+
+// Tail tiles: Y = act(sum_s slab[s][tile] * scale + bias + residual), fixed split order.
+// One workgroup per (tail tile, 1024 elements).
+__global__ void __launch_bounds__(256) conv_tail_reduce_kernel(
+    const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tiles_m,
+    int tiles_n, int Cout, int P, ConvEpi epi, float* __restrict__ Y) {
+  const int tile_elems = bm * kBN;
+  const int per_tile = tile_elems / 1024;
+  const int ti = blockIdx.x / per_tile;
+  int t = dp_tiles + ti;
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int nt = t % tiles_n;
+  const int img = t / tiles_n;
+  const size_t stride = (size_t)n_tail * tile_elems;
+  const float* S = slab + (size_t)ti * tile_elems;
+  const int e0 = (blockIdx.x % per_tile) * 1024;
+  for (int e = e0 + threadIdx.x; e < e0 + 1024; e += 256) {
+    const int co = mt * bm + e / kBN, p = nt * kBN + e % kBN;
+    if (co >= Cout || p >= P) continue;
+    float v = S[e];
+    for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
+    const size_t idx = ((size_t)img * Cout + co) * P + p;
+    if (epi.scale) v *= epi.scale[co];
+    if (epi.bias) v += epi.bias[co];
+    if (epi.residual) v += epi.residual[idx];
+    if (epi.relu) v = fmaxf(v, 0.f);
+    Y[idx] = v;
+  }
+}
+
+
+template <int AK, int NP, int MI>
+struct ConvGemm {
+  static constexpr int NPL = NP == 6 ? 3 : 2;
+  static constexpr int kBM = kWM * MI * 32;
+  static constexpr size_t kLds = 2 * NPL * (Img<AK>::PLANE + Img<0>::PLANE);
+  static TailPlan plan(int N, int C, int H, int W, int Cout) {
+    const int slots = slots_of(conv_gemm_bs_kernel<AK, NP, MI>, kLds);
+    const int tiles = div_up(Cout, kBM) * div_up(H * W, kBN) * N;
+    const int nchunks = div_up(C * 9, kTK);
+    // bf16 MFMA time of one whole tile per resident slot at ~50% of the dense peak
+    const double tile_s = 2.0 * kBM * kBN * kTK * NP * nchunks / (2516.6e12 * 0.5 / slots);
+    return plan_tail(tiles, nchunks, slots, tile_s, 4.0 * kBM * kBN);
+  }
+  static size_t ws_bytes(int N, int C, int H, int W, int Cout) {
+    const TailPlan p = plan(N, C, H, W, Cout);
+    const int tiles = div_up(Cout, kBM) * div_up(H * W, kBN) * N;
+    return p.ksplit > 1 ? (size_t)p.ksplit * (tiles - p.dp_tiles) * kBM * kBN * sizeof(float) : 0;
+  }
+  static int run(const float* X, const float* Wt, ConvEpi epi, float* Y, int N, int C, int H,
+                 int W, int Cout, float* ws, size_t ws_bytes_, hipStream_t s) {
+    const TailPlan p = plan(N, C, H, W, Cout);
+    if (ws_bytes_ < ws_bytes(N, C, H, W, Cout)) {
+      set_error("tlod_conv3x3_gemm_bs_f32: workspace too small");
+      return kWorkspace;
+    }
+    const int tiles_m = div_up(Cout, kBM), tiles_n = div_up(H * W, kBN);
+    const int n_tail = tiles_m * tiles_n * N - p.dp_tiles;
+    auto kern = conv_gemm_bs_kernel<AK, NP, MI>;
+    static bool attr = false;
+    if (!attr) {
+      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
+      attr = true;
+    }
+    const int nwg = p.dp_tiles + (p.ksplit > 1 ? n_tail * p.ksplit : 0);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, X, Wt, epi, Y, ws, N, C, H, W, Cout,
+                       tiles_m, tiles_n, p.dp_tiles, p.ksplit, p.cps);
+    TLOD_LAUNCH_CHECK();
+    if (p.ksplit > 1) {
+      hipLaunchKernelGGL(conv_tail_reduce_kernel, dim3(n_tail * (kBM * kBN / 1024)), dim3(256), 0, s,
+                         ws, p.ksplit, n_tail, p.dp_tiles, kBM, tiles_m, tiles_n, Cout, H * W, epi, Y);
+      TLOD_LAUNCH_CHECK();
+    }
+    return kOk;
+  }
+};
+
+template <typename F>
+auto with_conv_gemm(int w_layout, int nprod, F&& f) {
+  if (w_layout == 0) return nprod == 6 ? f(ConvGemm<1, 6, 4>{}) : f(ConvGemm<1, 3, 4>{});
+  return nprod == 6 ? f(ConvGemm<0, 6, 4>{}) : f(ConvGemm<0, 3, 4>{});
 }
 
 }  // namespace
@@ -343,9 +642,8 @@ using namespace tlod;
 extern "C" size_t tlod_gemm_bs_workspace_bytes(int M, int N, int K, int a_kcontig, int b_kcontig,
                                                int nprod) {
   if (M <= 0 || N <= 0 || K <= 0 || (nprod != 3 && nprod != 6)) return 0;
-  const int sp = with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod,
-                           [&](auto g) { return g.splits(M, N, K); });
-  return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
+  return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod,
+                   [&](auto g) { return g.ws_bytes(M, N, K); });
 }
 
 extern "C" int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c, int M,
@@ -357,5 +655,29 @@ extern "C" int tlod_gemm_bs_f32(const float* a, const float* b, const float* bia
   TLOD_CHECK_ARG((size_t)std::max(M, N) * K * 4 < (1ull << 31), "operand too large");
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
     return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+  });
+}
+
+extern "C" size_t tlod_conv3x3_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
+                                                       int w_layout, int nprod) {
+  if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0 || (nprod != 3 && nprod != 6)) return 0;
+  return with_conv_gemm(w_layout, nprod, [&](auto g) { return g.ws_bytes(N, Cin, H, W, Cout); });
+}
+
+extern "C" int tlod_conv3x3_gemm_bs_f32(const float* x, const float* w, int w_layout,
+                                        const float* scale, const float* bias,
+                                        const float* residual, float* y, int N, int Cin, int H,
+                                        int W, int Cout, int relu, int nprod, void* ws,
+                                        size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0 && x && w && y, "bad arguments");
+  TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
+  TLOD_CHECK_ARG(w_layout == 0 || w_layout == 1, "w_layout must be 0 or 1");
+  TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
+  // 32-bit buffer byte offsets
+  TLOD_CHECK_ARG((size_t)N * Cin * H * W * 4 < (1ull << 31) && (size_t)Cout * Cin * 9 * 4 < (1ull << 31),
+                 "operand too large");
+  return with_conv_gemm(w_layout, nprod, [&](auto g) {
+    return g.run(x, w, ConvEpi{scale, bias, residual, relu}, y, N, Cin, H, W, Cout,
+                 static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   });
 }

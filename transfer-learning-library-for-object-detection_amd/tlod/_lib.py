@@ -101,6 +101,10 @@ SIGNATURES = {
     "tlod_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "tlod_gemm_bs_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                  c_size_t, P]),
+    "tlod_conv3x3_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
+                                                        c_int]),
+    "tlod_conv3x3_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
+                                         c_int, c_int, c_int, P, c_size_t, P]),
     "tlod_stem_conv7x7s2_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),

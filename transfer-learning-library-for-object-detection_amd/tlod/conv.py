@@ -49,7 +49,8 @@ def conv_math():
                same normwise ~1e-7 vs fp64 as the f32-input MFMA; tests/test_conv_bs_gpu.py);
       "f32"  : the f32-input MFMA (exact f32 products);
       "bf16x3": 3 products (~5e-6 normwise), opt-in.
-    1x1 convs and wgrad use the f32-input MFMA in every mode."""
+    The 3x3 weight gradients follow it too (override: TLOD_WGRAD_MATH); 1x1 convs use the
+    f32-input MFMA in every mode."""
     m = os.environ.get("TLOD_CONV_MATH", "bf16x6")
     if m not in MATHS:
         raise ValueError(f"TLOD_CONV_MATH={m!r}: expected one of {MATHS}")
@@ -58,6 +59,36 @@ def conv_math():
 
 def _bs(KS, math):
     return KS == 3 and math != "f32"
+
+
+def _gemm_conv(KS, math, out_channels):
+    """3x3 split-bf16 convs with >= 256 output channels run as an implicit GEMM over
+    flattened pixels (tlod_conv3x3_gemm_bs_f32, 256x256 tiles); narrower ones keep the
+    patch-staged kernel (tlod_conv_fwd_bs_f32).  Opt-in (TLOD_CONV_GEMM=1): measured equal
+    to the patch-staged kernel in the DAF step (conv3_3 fwd 0.558 vs 0.553 ms)."""
+    return (_bs(KS, math) and out_channels >= 256
+            and os.environ.get("TLOD_CONV_GEMM", "0") != "0")
+
+
+def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind):
+    N, Cin, H, W = x.shape
+    y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
+    b = bias.detach().contiguous() if bias is not None else None
+    sc = scale.detach().contiguous() if scale is not None else None
+    res = residual.detach().contiguous() if residual is not None else None
+    if res is not None:
+        assert res.shape == y.shape, (res.shape, y.shape)
+    L = _lib.lib()
+    nprod = 6 if math == "bf16x6" else 3
+    ws = _lib.workspace(L.tlod_conv3x3_gemm_bs_workspace_bytes(N, Cin, H, W, Cout, w_layout, nprod),
+                        x.device, "conv")
+    shape = (N, Cin, H, W, Cout, 3) if kind == "fwd" else (N, Cout, H, W, Cin, 3)
+    _timed(kind, shape, lambda: _lib.check(
+        L.tlod_conv3x3_gemm_bs_f32(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc), _lib.ptr(b),
+                                   _lib.ptr(res), _lib.ptr(y), N, Cin, H, W, Cout, int(relu), nprod,
+                                   _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv3x3_gemm_bs"),
+        math)
+    return y
 
 
 def pack_bs(weight, dgrad):
@@ -103,6 +134,9 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=Non
     N, Cin, H, W = x.shape
     Cout, _, KS, _ = weight.shape
     math = conv_math() if math is None else math
+    if _gemm_conv(KS, math, Cout):
+        return _conv_gemm(x, weight.detach().contiguous(), 0, bias, relu, scale, residual, Cout,
+                          math, "fwd")
     if _bs(KS, math):
         return _conv_bs(x, pack_bs(weight, False) if wk is None else wk, bias, relu, scale,
                         residual, Cout, KS, math, "fwd")
@@ -145,6 +179,8 @@ def conv_dgrad(g, weight, wd=None, math=None):
     N, Cout, H, W = g.shape
     _, Cin, KS, _ = weight.shape
     math = conv_math() if math is None else math
+    if _gemm_conv(KS, math, Cin):
+        return _conv_gemm(g, pack_dgrad(weight), 1, None, False, None, None, Cin, math, "dgrad")
     if _bs(KS, math):
         # dgrad = the forward form over dy with the transposed, flipped pack
         return _conv_bs(g, pack_bs(weight, True) if wd is None else wd, None, False, None, None,
