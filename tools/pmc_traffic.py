@@ -11,8 +11,9 @@ import csv
 import json
 import sys
 
-CONV = ("conv_fwd_kernel", "conv_wgrad_kernel", "fwd_tail_reduce_kernel", "slab_reduce_kernel",
-        "relu_bwd_bias_kernel", "pack_fwd_kernel", "pack_dgrad_kernel")
+CONV = ("conv_fwd_kernel", "conv_wgrad_kernel", "conv_fwd_bs_kernel", "conv_wgrad_bs_kernel",
+        "fwd_tail_reduce_kernel", "slab_reduce_kernel", "relu_bwd_bias_kernel", "pack_fwd_kernel",
+        "pack_dgrad_kernel", "pack_bs_kernel")
 
 
 def total(path, counter):
@@ -22,7 +23,7 @@ def total(path, counter):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"]
-            key = next((k for k in CONV if k in name), None)
+            key = next((k for k in CONV if k + "<" in name or k + "(" in name), None)
             if key:
                 by[key] = by.get(key, 0.0) + float(r["Counter_Value"]) * 1024.0
     return by
