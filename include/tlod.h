@@ -202,14 +202,14 @@ int tlod_proposal_target_f32(const float* rois, int B, int R, const float* gt_bo
  * fwd/dgrad split the input channels over workgroups (deterministic slab reduction) when
  * the output tiles cannot fill the chip; *_workspace_bytes reports the slab size (0 when no
  * split is used).
- * relu_bwd_bias: g = dy * (y > 0) (y may be NULL: g = dy), db += sum over n,h,w of g
- *        (db may be NULL).  g may alias dy.
+ * relu_bwd_bias: g = dy * (y > 0) (y may be NULL: g = dy), db = sum over n,h,w of g
+ *        (written, not accumulated: no zero fill needed; db may be NULL).  g may alias dy.
  * fwd_ex: y = act(conv * scale[co] + bias[co] + residual) — the ResNet bottleneck epilogue
  *        (frozen BatchNorm folded to scale/bias, lib/DAF/resnet.py:261-284; identity or
  *        downsample branch added before the ReLU, resnet.py:94-97).  Any of scale, bias,
  *        residual may be NULL; residual (N,Cout,H,W) must not alias y.
  * relu_bwd_ex: g0 = dy * (y > 0); g = g0 * scale[c] (scale may be NULL); g_raw = g0 when
- *        g_raw != NULL (the residual branch's gradient); db += sum g0 when db != NULL. */
+ *        g_raw != NULL (the residual branch's gradient); db = sum g0 when db != NULL. */
 int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
                            tlod_stream_t stream);
 int tlod_conv_pack_dgrad_f32(const float* weight, int Cout, int Cin, int KS, float* wd,

@@ -1152,42 +1152,46 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ Wt, float* __restric
 // G0 = dY * (Y > 0) (when Y given); db[co] (+)= sum over n,p of G0; G = G0 * scale[co]
 // (scale: a folded frozen BatchNorm, optional); G0 also stored to Graw when given (the
 // residual branch of a bottleneck takes the unscaled gradient).  grid (Cout, N).
+// One workgroup per channel, looping over the N images: db[co] is written (not accumulated),
+// so the caller needs no zero fill, and the sum order is fixed (deterministic).
 __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restrict__ dY,
                                                             const float* __restrict__ Y,
                                                             const float* __restrict__ scale,
                                                             float* __restrict__ G,
                                                             float* __restrict__ Graw,
-                                                            float* __restrict__ db, int Cout,
-                                                            int HW) {
-  const int co = blockIdx.x, n = blockIdx.y;
-  const size_t base = ((size_t)n * Cout + co) * HW;
+                                                            float* __restrict__ db, int N,
+                                                            int Cout, int HW) {
+  const int co = blockIdx.x;
   const float sc = scale ? scale[co] : 1.f;
   float s = 0.f;
   const bool vec = (HW % 4) == 0;
-  if (vec) {
-    const float4* d4 = reinterpret_cast<const float4*>(dY + base);
-    const float4* y4 = Y ? reinterpret_cast<const float4*>(Y + base) : nullptr;
-    float4* g4 = reinterpret_cast<float4*>(G + base);
-    float4* r4 = Graw ? reinterpret_cast<float4*>(Graw + base) : nullptr;
-    for (int i = threadIdx.x; i < HW / 4; i += 256) {
-      float4 d = d4[i];
-      if (y4) {
-        const float4 y = y4[i];
-        d.x = y.x > 0.f ? d.x : 0.f; d.y = y.y > 0.f ? d.y : 0.f;
-        d.z = y.z > 0.f ? d.z : 0.f; d.w = y.w > 0.f ? d.w : 0.f;
+  for (int n = 0; n < N; ++n) {
+    const size_t base = ((size_t)n * Cout + co) * HW;
+    if (vec) {
+      const float4* d4 = reinterpret_cast<const float4*>(dY + base);
+      const float4* y4 = Y ? reinterpret_cast<const float4*>(Y + base) : nullptr;
+      float4* g4 = reinterpret_cast<float4*>(G + base);
+      float4* r4 = Graw ? reinterpret_cast<float4*>(Graw + base) : nullptr;
+      for (int i = threadIdx.x; i < HW / 4; i += 256) {
+        float4 d = d4[i];
+        if (y4) {
+          const float4 y = y4[i];
+          d.x = y.x > 0.f ? d.x : 0.f; d.y = y.y > 0.f ? d.y : 0.f;
+          d.z = y.z > 0.f ? d.z : 0.f; d.w = y.w > 0.f ? d.w : 0.f;
+        }
+        if (r4) r4[i] = d;
+        s += (d.x + d.y) + (d.z + d.w);
+        if (scale) { d.x *= sc; d.y *= sc; d.z *= sc; d.w *= sc; }
+        if (G != dY || y4 || scale) g4[i] = d;
       }
-      if (r4) r4[i] = d;
-      s += (d.x + d.y) + (d.z + d.w);
-      if (scale) { d.x *= sc; d.y *= sc; d.z *= sc; d.w *= sc; }
-      if (G != dY || y4 || scale) g4[i] = d;
-    }
-  } else {
-    for (int i = threadIdx.x; i < HW; i += 256) {
-      float d = dY[base + i];
-      if (Y) d = Y[base + i] > 0.f ? d : 0.f;
-      if (Graw) Graw[base + i] = d;
-      s += d;
-      G[base + i] = scale ? d * sc : d;
+    } else {
+      for (int i = threadIdx.x; i < HW; i += 256) {
+        float d = dY[base + i];
+        if (Y) d = Y[base + i] > 0.f ? d : 0.f;
+        if (Graw) Graw[base + i] = d;
+        s += d;
+        G[base + i] = scale ? d * sc : d;
+      }
     }
   }
   if (!db) return;
@@ -1195,7 +1199,7 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
   __shared__ float ws[4];
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(db + co, (ws[0] + ws[1]) + (ws[2] + ws[3]));
+  if (threadIdx.x == 0) db[co] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
 }
 
 // ======================================================================= launchers
@@ -1688,8 +1692,8 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
 extern "C" int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db,
                                       int N, int C, int HW, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0, "bad shape");
-  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C, N), dim3(256), 0, (hipStream_t)stream, dy, y,
-                     nullptr, g, nullptr, db, C, HW);
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, y,
+                     nullptr, g, nullptr, db, N, C, HW);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }
@@ -1699,8 +1703,8 @@ extern "C" int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float
                                     tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0 && dy && g, "bad arguments");
   TLOD_CHECK_ARG(g_raw != g || g_raw == nullptr, "g_raw must not alias g");
-  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C, N), dim3(256), 0, (hipStream_t)stream, dy, y,
-                     scale, g, g_raw, db, C, HW);
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, y,
+                     scale, g, g_raw, db, N, C, HW);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

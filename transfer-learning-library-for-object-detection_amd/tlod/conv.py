@@ -235,7 +235,7 @@ def relu_bwd_bias(dy, y=None, want_db=True):
     dy = dy.contiguous()
     N, C, H, W = dy.shape
     g = torch.empty_like(dy) if y is not None else dy
-    db = torch.zeros(C, dtype=torch.float32, device=dy.device) if want_db else None
+    db = torch.empty(C, dtype=torch.float32, device=dy.device) if want_db else None
     _lib.check(_lib.lib().tlod_relu_bwd_bias_f32(_lib.ptr(dy), _lib.ptr(y.contiguous() if y is not None else None),
                                                  _lib.ptr(g), _lib.ptr(db), N, C, H * W,
                                                  _lib.stream_of(dy)), "relu_bwd_bias")

@@ -27,7 +27,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..config import cfg
-from ..detector.losses import smooth_l1_loss
+from ..rpn.proposal import proposals_on_side_streams
+from ..detector.losses import smooth_l1_loss, weighted_loss_sum
 from ..rpn.rpn_head import _RPN
 from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, image_label
 from .daf import resnet as _daf_resnet
@@ -106,18 +107,21 @@ class _fasterRCNN(_DAFBase):
             hs = [rpn.head(f) for f in (base_feat, base_t, tgt_base_feat)]
 
         # ---- RPN, train mode, on the source image through both branches (:130-134)
-        rois_domain = rpn.RPN_proposal((hs[0][2].detach(), hs[0][3].detach(), im_info, "TRAIN"))
+        # target image: eval-mode RPN with TEST post-NMS top-N := the train count (:258-260,
+        # rois_domain.size(1)); the three proposal layers run on side streams while this
+        # stream computes the two RPN losses
+        cfg.TEST.RPN_POST_NMS_TOP_N = cfg.TRAIN.RPN_POST_NMS_TOP_N
+        pending = proposals_on_side_streams(rpn.RPN_proposal, [
+            (hs[0][2].detach(), hs[0][3].detach(), im_info, "TRAIN"),
+            (hs[1][2].detach(), hs[1][3].detach(), im_info, "TRAIN"),
+            (hs[2][2].detach(), hs[2][3].detach(), tgt_im_info.detach(), "TEST")])
         l_cls1, l_box1, _ = rpn.losses(hs[0][0], hs[0][1], hs[0][3], gt_boxes, im_info, num_boxes,
                                        rng=self.replay_rng)
-        rois_domain_t = rpn.RPN_proposal((hs[1][2].detach(), hs[1][3].detach(), im_info, "TRAIN"))
         l_cls2, l_box2, _ = rpn.losses(hs[1][0], hs[1][1], hs[1][3], gt_boxes, im_info, num_boxes,
                                        rng=self.replay_rng)
         rpn_loss_cls = l_cls1 + l_cls2
         rpn_loss_bbox = l_box1 + l_box2
-        # target image: eval-mode RPN with TEST post-NMS top-N := train count (:258-260)
-        cfg.TEST.RPN_POST_NMS_TOP_N = rois_domain.size(1)
-        tgt_rois = rpn.RPN_proposal((hs[2][2].detach(), hs[2][3].detach(),
-                                     tgt_im_info.detach(), "TEST"))
+        rois_domain, rois_domain_t, tgt_rois = pending.join()
         if self.capture is not None:
             self.capture.update(s_rois=rois_domain.detach().clone(),
                                 st_rois=rois_domain_t.detach().clone(),
@@ -191,10 +195,9 @@ class _fasterRCNN(_DAFBase):
         """methods/ATF/ATF_train.py:405-408 (image DA weighted 7x)."""
         (_, _, _, rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, _, DA_img,
          tgt_DA_img, DA_ins, tgt_DA_ins) = out
-        return (rpn_loss_cls.mean() + rpn_loss_box.mean() + RCNN_loss_cls.mean()
-                + RCNN_loss_bbox.mean()
-                + lamda * (7 * DA_img.mean() + DA_ins.mean() + 7 * tgt_DA_img.mean()
-                           + tgt_DA_ins.mean()))
+        return weighted_loss_sum(
+            (rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, DA_img, DA_ins, tgt_DA_img,
+             tgt_DA_ins), (1, 1, 1, 1, lamda * 7, lamda, lamda * 7, lamda))
 
 
 class vgg16(_fasterRCNN):

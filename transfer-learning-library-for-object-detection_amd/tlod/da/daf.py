@@ -21,10 +21,11 @@ import torch.nn.functional as F
 from ..config import cfg
 from ..conv import Conv2d
 from ..linear import Linear
-from ..detector.losses import smooth_l1_loss
+from ..detector.losses import smooth_l1_loss, weighted_loss_sum
 from ..detector.vgg16 import vgg16_base, vgg16_top
 from ..roi_align import RoIAlignAvg
 from ..roi_pool import _RoIPooling
+from ..rpn.proposal import proposals_on_side_streams
 from ..rpn.proposal_target import _ProposalTargetLayer
 from ..rpn.rpn_head import _RPN
 
@@ -39,7 +40,7 @@ class GRLayer(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return g.neg() * ctx.alpha, None
+        return g * (-ctx.alpha), None  # = g.neg() * alpha bit for bit (negation is exact)
 
 
 def grad_reverse(x, alpha=0.1):
@@ -174,13 +175,19 @@ class _fasterRCNN(nn.Module):
             s_score, s_score_r, s_prob, s_bbox = self.RCNN_rpn.head(base_feat)
             _, _, t_prob, t_bbox = self.RCNN_rpn.head(tgt_base_feat)
 
-        # source RPN in train mode (faster_rcnn.py:62-63)
+        # source RPN in train mode (faster_rcnn.py:62-63); target RPN in eval mode
+        # (faster_rcnn.py:140-142): TEST proposals, no losses.  The two proposal layers run
+        # on side streams while this stream does the anchor target, RPN losses and the
+        # image-level DA head (independent of the proposals).
         rpn = self.RCNN_rpn
-        rois = rpn.RPN_proposal((s_prob.detach(), s_bbox.detach(), im_info, "TRAIN"))
+        pending = proposals_on_side_streams(rpn.RPN_proposal, [
+            (s_prob.detach(), s_bbox.detach(), im_info, "TRAIN"),
+            (t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST")])
         rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes, im_info,
                                                     num_boxes, rng=self.replay_rng)
-        # target RPN in eval mode (faster_rcnn.py:140-142): TEST proposals, no losses
-        tgt_rois = rpn.RPN_proposal((t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST"))
+        if same:
+            score_img2, _ = self.RCNN_imageDA(base2, need_backprop.new_ones(2))
+        rois, tgt_rois = pending.join()
         if self.capture is not None:
             self.capture.update(s_rois=rois.detach().clone(), t_rois=tgt_rois.detach().clone())
 
@@ -209,7 +216,6 @@ class _fasterRCNN(nn.Module):
 
         # DA heads (faster_rcnn.py:181-220)
         if same:
-            score_img2, _ = self.RCNN_imageDA(base2, need_backprop.new_ones(2))
             base_score, tgt_base_score = score_img2[:1], score_img2[1:]
             ins2, _ = self.RCNN_instanceDA(feat2, need_backprop.new_ones(1))
             ins_s, ins_t = ins2[:n_s], ins2[n_s:]
@@ -231,10 +237,9 @@ class _fasterRCNN(nn.Module):
         """methods/DAF/DAF_train.py:397-400."""
         (_, _, _, rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, _, DA_img, DA_ins,
          tgt_DA_img, tgt_DA_ins, DA_cst, tgt_DA_cst) = out
-        return (rpn_loss_cls.mean() + rpn_loss_box.mean() + RCNN_loss_cls.mean()
-                + RCNN_loss_bbox.mean()
-                + lamda * (DA_img.mean() + DA_ins.mean() + tgt_DA_img.mean() + tgt_DA_ins.mean()
-                           + DA_cst.mean() + tgt_DA_cst.mean()))
+        return weighted_loss_sum(
+            (rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, DA_img, DA_ins, tgt_DA_img,
+             tgt_DA_ins, DA_cst, tgt_DA_cst), (1, 1, 1, 1) + (lamda,) * 6)
 
     def _init_weights(self):
         """faster_rcnn.py:227-243 (normal_init, truncated=False)."""

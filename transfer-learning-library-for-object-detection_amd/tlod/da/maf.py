@@ -18,7 +18,9 @@ import torch.nn.functional as F
 
 from .. import _lib
 from ..conv import Conv2d
+from ..detector.losses import weighted_loss_sum
 from ..linear import Linear
+from ..rpn.proposal import proposals_on_side_streams
 from .daf import _ImageDA, _fasterRCNN as _DAFBase, grad_reverse, image_label
 from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
@@ -180,10 +182,13 @@ class _fasterRCNN(_DAFBase):
             _, _, t_prob, t_bbox = self.RCNN_rpn.head(feats[1][2])
 
         rpn = self.RCNN_rpn
-        rois = rpn.RPN_proposal((s_prob.detach(), s_bbox.detach(), im_info, "TRAIN"))
+        # proposal layers on side streams, overlapping the anchor target / RPN losses
+        pending = proposals_on_side_streams(rpn.RPN_proposal, [
+            (s_prob.detach(), s_bbox.detach(), im_info, "TRAIN"),
+            (t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST")])
         rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes, im_info,
                                                     num_boxes, rng=self.replay_rng)
-        tgt_rois = rpn.RPN_proposal((t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST"))
+        rois, tgt_rois = pending.join()
         if self.capture is not None:
             self.capture.update(s_rois=rois.detach().clone(), t_rois=tgt_rois.detach().clone())
 
@@ -246,10 +251,9 @@ class _fasterRCNN(_DAFBase):
         """methods/MAF/MAF_train.py:415-418."""
         (_, _, _, rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, _, DA_img, DA_ins,
          tgt_DA_img, tgt_DA_ins) = out
-        return (rpn_loss_cls.mean() + rpn_loss_box.mean() + RCNN_loss_cls.mean()
-                + RCNN_loss_bbox.mean()
-                + lamda * (DA_img.mean() + alpha * DA_ins.mean() + tgt_DA_img.mean()
-                           + alpha * tgt_DA_ins.mean()))
+        return weighted_loss_sum(
+            (rpn_loss_cls, rpn_loss_box, RCNN_loss_cls, RCNN_loss_bbox, DA_img, DA_ins, tgt_DA_img,
+             tgt_DA_ins), (1, 1, 1, 1, lamda, lamda * alpha, lamda, lamda * alpha))
 
 
 class vgg16(_fasterRCNN):
