@@ -289,6 +289,25 @@ int tlod_conv3x3_gemm_bs_f32(const float* x, const float* w, int w_layout, const
                              int H, int W, int Cout, int relu, int nprod, void* ws,
                              size_t ws_bytes, tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ Max pooling
+ * Replaces: nn.MaxPool2d(kernel_size=2, stride=2) (floor mode) in RCNN_base (torchvision
+ *   vgg16().features, lib/DAF/vgg16.py:49) and, backward, its routing fused with the
+ *   preceding conv's ReLU backward.
+ * maxpool2x2: y (N,C,H/2,W/2) = window max, torch's tie rule (first max, NaN wins).
+ * maxpool2x2_relu_bwd: y = the pool input (the conv's ReLU output, (N,C,H,W)), dp the
+ *   pooled gradient; g (N,C,H,W) = dp routed to each window's argmax (recomputed from y with
+ *   max_pool2d's rule) where y > 0, else 0; db[c] = sum of g (written; db may be NULL).
+ * conv_fwd_bs_pool: tlod_conv_fwd_bs_f32 followed by maxpool2x2 in the kernel epilogue
+ *   (the full-resolution map is never written): y_pooled (N,Cout,H/2,W/2).  For frozen
+ *   layers whose output only feeds the pool (VGG16 conv1_2 / conv2_2). */
+int tlod_maxpool2x2_f32(const float* x, int N, int C, int H, int W, float* y,
+                        tlod_stream_t stream);
+int tlod_maxpool2x2_relu_bwd_f32(const float* dp, const float* y, int N, int C, int H, int W,
+                                 float* g, float* db, tlod_stream_t stream);
+int tlod_conv_fwd_bs_pool_f32(const float* x, const void* wp, const float* scale,
+                              const float* bias, float* y_pooled, int N, int Cin, int H, int W,
+                              int Cout, int KS, int relu, int nprod, tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ ResNet101 extras
  * Replaces: cuDNN for the ResNet101 stem conv1 7x7/2 + bn1 + relu (lib/DAF/resnet.py:107-110,
  *   frozen, forward only) and the stride-2 1x1 convolutions of the caffe-style bottleneck

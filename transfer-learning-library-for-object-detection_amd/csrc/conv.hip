@@ -65,6 +65,8 @@ struct Epi {
   const float* bias;
   const float* residual;
   int relu;
+  float* pool;  // conv_fwd_bs_kernel (2D tiles, no split-K) only: write max_pool2d(2, 2) of
+                // the result here (N, Cout, H/2, W/2) instead of the full map
 };
 
 // ======================================================================= forward
@@ -585,9 +587,41 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
         }
     return;
   }
+  const bool has_scale = epi.scale != nullptr;
+  if constexpr (!BAND && NJ == 2) {
+    if (epi.pool) {
+      // Fused max_pool2d(kernel 2, stride 2, floor): rows (j = 0, 1) are a window's two
+      // rows, lanes (l32, l32 ^ 1) its two columns.  The window order and the update rule
+      // (val > max || isnan(val)) are torch's max_pool2d forward, so the values are identical.
+      const int Hp = H / 2, Wp = W / 2;
+      float* Pn = epi.pool + (size_t)n * Cout * Hp * Wp;
+      const int hp = (h0 + wn * NJ) / 2, wp = (w0 + l32) / 2;
+      const bool writer = (l32 & 1) == 0 && hp < Hp && wp < Wp;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ml = wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+          float v[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            v[j] = acc[i][j][r];
+            if (has_scale) v[j] *= scale_s[ml];
+            v[j] += bias_s[ml];
+            if (epi.relu) v[j] = fmaxf(v[j], 0.f);
+          }
+          const float c0 = __shfl_xor(v[0], 1), c1 = __shfl_xor(v[1], 1);
+          float m = v[0];
+          if (c0 > m || __builtin_isnan(c0)) m = c0;
+          if (v[1] > m || __builtin_isnan(v[1])) m = v[1];
+          if (c1 > m || __builtin_isnan(c1)) m = c1;
+          if (writer && m0 + ml < Cout) Pn[((size_t)(m0 + ml) * Hp + hp) * Wp + wp] = m;
+        }
+      return;
+    }
+  }
   float* Yn = Y + (size_t)n * Cout * H * W;
   const float* Rn = epi.residual ? epi.residual + (size_t)n * Cout * H * W : nullptr;
-  const bool has_scale = epi.scale != nullptr;
   const int w = w0 + l32;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -1244,10 +1278,11 @@ static int resident_slots(K kern, int threads, size_t lds) {
 // through HBM.  Cost model in seconds: tiles at ~65% of the f32 MFMA peak per slot,
 // slab traffic (k writes + k reads + 1 write per tail tile) at 4 TB/s, 6 us per reduce.
 static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int nchunks,
-                             double tile_flops, int tile_elems, int slots) {
+                             double tile_flops, int tile_elems, int slots, bool allow_split = true) {
   FwdPlan p{tiles_m, tiles_w, tiles_h, 0, 1, nchunks, N};
   const long long T = (long long)tiles_m * tiles_w * tiles_h * N;
   p.dp_tiles = (int)T;
+  if (!allow_split) return p;
   const double tile_s = tile_flops / (157.3e12 * 0.65 / slots);
   double best = (double)((T + slots - 1) / slots) * tile_s;
   const int kmax = std::min(8, nchunks / 2);
@@ -1364,7 +1399,7 @@ static bool use_band(int H, int W) {
 }
 
 template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
-static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout) {
+static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_split = true) {
   using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
   static const int slots = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>, C::NT,
                                           C::LDS_BYTES);
@@ -1374,7 +1409,7 @@ static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout) {
   const int th = BAND ? 1 : div_up(H, C::TH);
   return plan_schedule(div_up(Cout, C::BM), tw, th, N, nchunks,
                        2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
-                       C::BM * C::TH * C::TW, slots);
+                       C::BM * C::TH * C::TW, slots, allow_split);
 }
 
 template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
@@ -1382,7 +1417,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
                          int Cin, int H, int W, int Cout, float* slab, size_t slab_bytes,
                          hipStream_t s) {
   using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
-  const FwdPlan p = plan_fwd_bs<WM, WN, MI, NJ, NP, BAND>(N, Cin, H, W, Cout);
+  const FwdPlan p = plan_fwd_bs<WM, WN, MI, NJ, NP, BAND>(N, Cin, H, W, Cout, epi.pool == nullptr);
   const long long nwg = (long long)p.dp_tiles + (long long)p.n_tail() * (p.ksplit > 1 ? p.ksplit : 0);
   TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
   if (p.ksplit > 1 && slab_bytes < p.slab_bytes(C::BM, C::TH)) {
@@ -1431,7 +1466,7 @@ static int conv_fwd_bs_dispatch(const float* X, const unsigned short* Wp, Epi ep
     return launch_fwd_bs<WM_, WN_, MI_, NJ_, NP_, BAND_>(X, Wp, epi, Y, N, Cin, H, W, Cout,     \
                                                          slab, sb, s);                          \
   } while (0)
-  const bool band = use_band(H, W);
+  const bool band = use_band(H, W) && epi.pool == nullptr;  // pooling: 2D tiles
   if (nprod == 6 && band) TLOD_BS_CFG(1, 8, 2, 2, 6, true);
   if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6, false);
   if (band) TLOD_BS_CFG(1, 8, 2, 2, 3, true);
@@ -1746,4 +1781,15 @@ extern "C" int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float*
   return conv_fwd_bs_dispatch(x, (const unsigned short*)wp, Epi{scale, bias, residual, relu}, y,
                               N, Cin, H, W, Cout, KS, nprod, (float*)ws, ws_bytes,
                               (hipStream_t)stream);
+}
+
+extern "C" int tlod_conv_fwd_bs_pool_f32(const float* x, const void* wp, const float* scale,
+                                         const float* bias, float* y_pooled, int N, int Cin,
+                                         int H, int W, int Cout, int KS, int relu, int nprod,
+                                         tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H >= 2 && W >= 2 && Cout > 0 && y_pooled, "bad shape");
+  Epi e{scale, bias, nullptr, relu};
+  e.pool = y_pooled;
+  return conv_fwd_bs_dispatch(x, (const unsigned short*)wp, e, nullptr, N, Cin, H, W, Cout, KS,
+                              nprod, nullptr, 0, (hipStream_t)stream);
 }

@@ -105,6 +105,10 @@ SIGNATURES = {
                                                         c_int]),
     "tlod_conv3x3_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, P, c_size_t, P]),
+    "tlod_maxpool2x2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_maxpool2x2_relu_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),
+    "tlod_conv_fwd_bs_pool_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                          c_int, c_int, P]),
     "tlod_stem_conv7x7s2_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),

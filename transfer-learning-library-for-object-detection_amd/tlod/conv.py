@@ -298,6 +298,74 @@ class ConvBNFunction(torch.autograd.Function):
         return dx, dw, None, None, g_raw, None
 
 
+def maxpool2x2(x):
+    """nn.MaxPool2d(2, 2) (floor mode) forward in libtlod (tlod_maxpool2x2_f32)."""
+    x = x.contiguous()
+    N, C, H, W = x.shape
+    y = torch.empty((N, C, H // 2, W // 2), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().tlod_maxpool2x2_f32(_lib.ptr(x), N, C, H, W, _lib.ptr(y),
+                                              _lib.stream_of(x)), "maxpool2x2")
+    return y
+
+
+def maxpool_relu_bwd(dp, y, want_db=True):
+    """Gradient through max_pool2d(2, 2) and the ReLU whose output y the pool read:
+    g = dp routed to each window's argmax where y > 0; db = sum g."""
+    dp = dp.contiguous()
+    N, C, H, W = y.shape
+    g = torch.empty_like(y)
+    db = torch.empty(C, dtype=torch.float32, device=y.device) if want_db else None
+    _lib.check(_lib.lib().tlod_maxpool2x2_relu_bwd_f32(_lib.ptr(dp), _lib.ptr(y), N, C, H, W,
+                                                       _lib.ptr(g), _lib.ptr(db),
+                                                       _lib.stream_of(y)), "maxpool_relu_bwd")
+    return g, db
+
+
+def conv_fwd_pool(x, weight, bias, math=None):
+    """max_pool2d(relu(conv(x) + bias), 2, 2) with the pooling in the conv epilogue (split-bf16
+    3x3, tlod_conv_fwd_bs_pool_f32): the full-resolution map is never written.  Forward only
+    (frozen layers); other maths pool in a separate kernel."""
+    _check(x, weight)
+    x = x.contiguous()
+    N, Cin, H, W = x.shape
+    Cout, _, KS, _ = weight.shape
+    math = conv_math() if math is None else math
+    if not _bs(KS, math):
+        return maxpool2x2(conv_fwd(x, weight, bias, True, math=math))
+    y = torch.empty((N, Cout, H // 2, W // 2), dtype=torch.float32, device=x.device)
+    b = bias.detach().contiguous() if bias is not None else None
+    nprod = 6 if math == "bf16x6" else 3
+    wp = pack_bs(weight, False)
+    _timed("fwd", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
+        _lib.lib().tlod_conv_fwd_bs_pool_f32(_lib.ptr(x), _lib.ptr(wp), None, _lib.ptr(b),
+                                             _lib.ptr(y), N, Cin, H, W, Cout, KS, 1, nprod,
+                                             _lib.stream_of(x)), "conv_fwd_bs_pool"), math)
+    return y
+
+
+class ConvPoolFunction(torch.autograd.Function):
+    """conv + bias + ReLU + max_pool2d(2, 2) as one autograd node: the backward routes the
+    pooled gradient through the recomputed argmax and the ReLU mask in one kernel
+    (tlod_maxpool2x2_relu_bwd_f32) — no index tensor, no full-size pool gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = conv_fwd(x, weight, bias, True)
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, y)
+        return maxpool2x2(y)
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, weight, y = ctx.saved_tensors
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        g, db = maxpool_relu_bwd(dp, y, want_db=need_b)
+        dx = conv_dgrad(g, weight) if need_x else None
+        dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
+        return dx, dw, db
+
+
 class Conv2d(nn.Conv2d):
     """nn.Conv2d-compatible (stride 1, padding k//2) with the libtlod kernels; optional
     fused ReLU."""
@@ -310,8 +378,17 @@ class Conv2d(nn.Conv2d):
         if stride != 1 or padding != k // 2 or k not in (1, 3):
             raise NotImplementedError("tlod.Conv2d: stride 1, 'same' padding, 1x1/3x3 only")
         self.relu = relu
+        self.pool = False  # set by the VGG16 builder: max_pool2d(2, 2) of the ReLU output
 
     def forward(self, x):
+        if self.pool:
+            assert self.relu
+            needs_grad = torch.is_grad_enabled() and (
+                x.requires_grad or self.weight.requires_grad
+                or (self.bias is not None and self.bias.requires_grad))
+            if not needs_grad:
+                return conv_fwd_pool(x, self.weight, self.bias)
+            return ConvPoolFunction.apply(x, self.weight, self.bias)
         if self.out_channels % 4:
             # GEMM-library path for the tiny 1x1 heads (e.g. 512->2 of _ImageDA.Conv2)
             assert self.kernel_size[0] == 1
@@ -321,7 +398,8 @@ class Conv2d(nn.Conv2d):
         return ConvFunction.apply(x, self.weight, self.bias, self.relu)
 
     def extra_repr(self):
-        return super().extra_repr() + (", relu=True" if self.relu else "")
+        return super().extra_repr() + (", relu=True" if self.relu else "") + \
+            (", maxpool2x2" if self.pool else "")
 
 
 def vgg_init_(conv):

@@ -203,6 +203,8 @@ class _fasterRCNN(_DAFBase):
 class vgg16(_fasterRCNN):
     """lib/ATF/vgg16.py:20-79."""
 
+    FUSE_POOLS = (1, 2)  # the DA taps read conv3 / conv4 before pools 3 / 4
+
     def __init__(self, classes, pretrained=False, class_agnostic=False):
         self.dout_base_model = 512
         self.instance_dim = 4096

@@ -267,8 +267,12 @@ class vgg16(_fasterRCNN):
         self.class_agnostic = class_agnostic
         _fasterRCNN.__init__(self, classes, class_agnostic)
 
+    # max-pools folded into the preceding conv (tlod.detector.vgg16.vgg16_base); MAF / ATF,
+    # whose DA taps read the conv3 / conv4 outputs, keep pools 3 and 4 separate
+    FUSE_POOLS = (1, 2, 3, 4)
+
     def _init_modules(self):
-        self.RCNN_base = vgg16_base()
+        self.RCNN_base = vgg16_base(fuse_pools=self.FUSE_POOLS)
         self.RCNN_top = vgg16_top()
         self.RCNN_cls_score = nn.Linear(4096, self.n_classes)
         self.RCNN_bbox_pred = nn.Linear(4096, 4 if self.class_agnostic else 4 * self.n_classes)

@@ -260,6 +260,8 @@ class vgg16(_fasterRCNN):
     """lib/MAF/vgg16.py:20-70: RCNN_base plus the conv3 / conv34 / conv45 views of the
     same modules (features[:16], [16:23], [23:-1])."""
 
+    FUSE_POOLS = (1, 2)  # the DA taps read conv3 / conv4 before pools 3 / 4
+
     def __init__(self, classes, pretrained=False, class_agnostic=False):
         self.dout_base_model = 512
         self.instance_dim = 4096

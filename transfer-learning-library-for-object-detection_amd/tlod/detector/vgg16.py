@@ -20,11 +20,22 @@ VGG16_SPLITS = (10, 16, 23)
 VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512]
 
 
-def vgg16_base(frozen_layers=10):
-    layers, cin = [], 3
+def vgg16_base(frozen_layers=10, fuse_pools=(1, 2)):
+    """RCNN_base with the max-pools listed in ``fuse_pools`` (1-4, in order) folded into the
+    preceding conv module (Conv2d.pool; the MaxPool2d slot becomes nn.Identity, so indices and
+    state_dict keys are unchanged).  Pools 1/2 follow frozen convs whose output feeds nothing
+    else (the conv epilogue pools, the full map is never written); pools 3/4 fold only where
+    no DA tap reads the conv3 / conv4 outputs (DAF), routing the backward through the fused
+    argmax + ReLU kernel."""
+    layers, cin, npool = [], 3, 0
     for v in VGG16_CFG:
         if v == "M":
-            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            npool += 1
+            if npool in fuse_pools:
+                layers[-2].pool = True
+                layers.append(nn.Identity())
+            else:
+                layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
         else:
             conv = Conv2d(cin, v, 3, relu=True)
             vgg_init_(conv)
