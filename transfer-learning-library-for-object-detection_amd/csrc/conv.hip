@@ -42,6 +42,11 @@ namespace tlod {
 #ifndef TLOD_MID_STORE
 #define TLOD_MID_STORE 1
 #endif
+// Split-bf16 forward: pair the 9 taps across consecutive input-channel chunks instead of
+// padding each chunk to 10 tap slots (0 = pad, for A/B).
+#ifndef TLOD_TAP_PAIRING
+#define TLOD_TAP_PAIRING 1
+#endif
 #ifndef TLOD_CONV_OCC
 #define TLOD_CONV_OCC __attribute__((amdgpu_waves_per_eu(2, 4)))
 #endif
@@ -421,13 +426,13 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 
   // ---- operand byte offsets inside one LDS buffer
   const int a_base = (wm * MI * 32 + l32) * C::AROW + 16 * khalf;
-  int b_off[C::STEPS];
-#pragma unroll
-  for (int st = 0; st < C::STEPS; ++st) {
-    const int tap = min(2 * st + khalf, 8);
-    b_off[st] = C::NPL * C::A_PLANE + (BAND ? (tap / 3 - 1) * PWr + tap % 3 - 1
-                                            : (wn * NJ + tap / 3) * C::PW + l32 + tap % 3) * 16;
-  }
+  // B operand byte offset of tap t inside one buffer = b_lane (per lane) + tap_c(t) (uniform)
+  const int b_lane = C::NPL * C::A_PLANE + (BAND ? 0 : (wn * NJ * C::PW + l32) * 16);
+  auto tap_c = [&](int tap) {
+    return (BAND ? (tap / 3 - 1) * PWr + tap % 3 - 1 : (tap / 3) * C::PW + tap % 3) * 16;
+  };
+  // offset of the pair (t0 for lanes 0-31, t1 for lanes 32-63)
+  auto pair_off = [&](int t0, int t1) { return b_lane + (khalf ? tap_c(t1) : tap_c(t0)); };
   // band: this lane's pixel of column block j sits at patch position (h - h0 + 1, w + 1)
   int b_pix[NJ];
 #pragma unroll
@@ -532,43 +537,77 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
     load_chunk(c_begin);
     store_chunk(smem);
   }
+  if (c_begin + 1 < c_end) load_chunk(c_begin + 1);
   __syncthreads();
 
-  for (int ch = c_begin; ch < c_end; ++ch) {
-    const int it = ch - c_begin;
+  // one k-step: A at per-lane byte offset aoff, B at boff (+ the lane's pixel offset)
+  auto step = [&](const unsigned char* buf, int aoff, int boff) {
+    u32x4 a[MI][3], b[NJ][3];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        a[i][pl] = *reinterpret_cast<const u32x4*>(buf + aoff + pl * C::A_PLANE + i * 32 * C::AROW);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        b[j][pl] = *reinterpret_cast<const u32x4*>(buf + boff + pl * C::B_PLANE + b_pix[j]);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (NP == 6) {
+          acc[i][j] = mfma_bf16(a[i][2], b[j][0], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[i][1], b[j][1], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[i][0], b[j][2], acc[i][j]);
+        }
+        acc[i][j] = mfma_bf16(a[i][1], b[j][0], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[i][0], b[j][1], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[i][0], b[j][0], acc[i][j]);
+      }
+  };
+
+  // Tap pairing over chunk pairs (no zero-pad MFMA work): the 18 (chunk, tap) units of the
+  // pair (c, c+1) — chunk c in LDS buffer 0, chunk c+1 in buffer 1 — are consumed two per
+  // k-step, unit u = 2s + khalf, so 9 k-steps cover 2 chunks instead of 10.  Chunk c+1 is
+  // stored at step 2 and made visible before step 4 (the step that straddles the buffers);
+  // chunk c+2 is stored into buffer 0 at step 6, after a barrier that retires step 4's
+  // reads of it.  A lone last chunk runs (0,1) .. (6,7), (8, pad): the pad weights are 0.
+  const int a_row = a_base - 16 * khalf;
+  auto unit_a = [&](int u) { return (u >= 9 ? C::BUF : 0) + 16 * (u % 9); };
+  auto unit_b = [&](int u) { return (u >= 9 ? C::BUF : 0) + tap_c(u % 9); };
+  int c = c_begin;
+  if (TLOD_TAP_PAIRING) {
+    for (; c + 1 < c_end; c += 2) {
+      const bool more2 = c + 2 < c_end;
+#pragma unroll
+      for (int st = 0; st < 9; ++st) {
+        if (st == 2) {
+          store_chunk(smem + C::BUF);
+          if (more2) load_chunk(c + 2);
+        }
+        if (st == 4 || st == 5) __syncthreads();
+        if (st == 6 && more2) {
+          store_chunk(smem);
+          if (c + 3 < c_end) load_chunk(c + 3);
+        }
+        step(smem, a_row + (khalf ? unit_a(2 * st + 1) : unit_a(2 * st)),
+             b_lane + (khalf ? unit_b(2 * st + 1) : unit_b(2 * st)));
+      }
+      __syncthreads();
+    }
+  }
+  for (; c < c_end; ++c) {  // lone last chunk (tap pairing) or every chunk (pad mode)
+    const int it = c - c_begin;
+    const bool more = c + 1 < c_end;
     const unsigned char* buf = smem + (it & 1) * C::BUF;
-    const bool more = ch + 1 < c_end;
-    if (more) load_chunk(ch + 1);
 #pragma unroll
     for (int st = 0; st < C::STEPS; ++st) {
-      if (TLOD_MID_STORE && more && st == C::STEPS / 2) store_chunk(smem + ((it + 1) & 1) * C::BUF);
-      u32x4 a[MI][3], b[NJ][3];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int pl = 0; pl < C::NPL; ++pl)
-          a[i][pl] = *reinterpret_cast<const u32x4*>(buf + a_base + pl * C::A_PLANE +
-                                                     i * 32 * C::AROW + 32 * st);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int pl = 0; pl < C::NPL; ++pl)
-          b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_off[st] + pl * C::B_PLANE + b_pix[j]);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          if constexpr (NP == 6) {
-            acc[i][j] = mfma_bf16(a[i][2], b[j][0], acc[i][j]);
-            acc[i][j] = mfma_bf16(a[i][1], b[j][1], acc[i][j]);
-            acc[i][j] = mfma_bf16(a[i][0], b[j][2], acc[i][j]);
-          }
-          acc[i][j] = mfma_bf16(a[i][1], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[i][0], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[i][0], b[j][0], acc[i][j]);
-        }
+      if (more && st == 2) store_chunk(smem + ((it + 1) & 1) * C::BUF);
+      step(buf, a_base + 32 * st, pair_off(min(2 * st, 8), min(2 * st + 1, 8)));
     }
-    if (!TLOD_MID_STORE && more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
+    if (more && c + 2 < c_end) load_chunk(c + 2);
     __syncthreads();
   }
 
