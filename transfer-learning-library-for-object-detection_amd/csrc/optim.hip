@@ -13,14 +13,33 @@
 
 namespace tlod {
 
+// 16-B vector path when the chunk's pointers are 16-B aligned and its count a multiple of
+// 4 (the grads can be views into the DP reducer's flat buckets at any float offset).
+__device__ __forceinline__ bool vec4_ok(const void* a, const void* b, const void* c,
+                                        long long n) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+           reinterpret_cast<uintptr_t>(c)) & 15) == 0 && (n & 3) == 0;
+}
+
 __global__ void __launch_bounds__(256) sgd_sumsq_kernel(const tlod_sgd_chunk* __restrict__ chunks,
                                                         float* __restrict__ partials) {
   const tlod_sgd_chunk c = chunks[blockIdx.x];
-  float s = 0.f;
-  for (long long i = threadIdx.x; i < c.count; i += 256) {
-    const float g = c.grad[i];
-    s += g * g;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (vec4_ok(c.grad, c.grad, c.grad, c.count)) {
+    const float4* g4 = reinterpret_cast<const float4*>(c.grad);
+    const long long n4 = c.count / 4;
+#pragma unroll 4
+    for (long long i = threadIdx.x; i < n4; i += 256) {
+      const float4 g = g4[i];
+      s0 += g.x * g.x; s1 += g.y * g.y; s2 += g.z * g.z; s3 += g.w * g.w;
+    }
+  } else {
+    for (long long i = threadIdx.x; i < c.count; i += 256) {
+      const float g = c.grad[i];
+      s0 += g * g;
+    }
   }
+  float s = (s0 + s1) + (s2 + s3);
   for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
   __shared__ float ws[4];
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
@@ -46,18 +65,41 @@ __global__ void __launch_bounds__(256) sgd_norm_kernel(const float* __restrict__
   }
 }
 
+__device__ __forceinline__ void sgd1(float g, float& p, float& b, float scale, float wd,
+                                     float lr, float momentum) {
+  const float d = g * scale + wd * p;
+  b = momentum * b + d;
+  p = p - lr * b;
+}
+
 __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* __restrict__ chunks,
                                                          const float* __restrict__ norm_scale,
                                                          float momentum) {
   const tlod_sgd_chunk c = chunks[blockIdx.x];
   const float scale = norm_scale[1];
+  if (vec4_ok(c.grad, c.param, c.momentum_buf, c.count)) {
+    const float4* __restrict__ g4 = reinterpret_cast<const float4*>(c.grad);
+    float4* __restrict__ p4 = reinterpret_cast<float4*>(c.param);
+    float4* __restrict__ b4 = reinterpret_cast<float4*>(c.momentum_buf);
+    const long long n4 = c.count / 4;
+#pragma unroll 2
+    for (long long i = threadIdx.x; i < n4; i += 256) {
+      const float4 g = g4[i];
+      float4 p = p4[i], b = b4[i];
+      sgd1(g.x, p.x, b.x, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.y, p.y, b.y, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.z, p.z, b.z, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.w, p.w, b.w, scale, c.weight_decay, c.lr, momentum);
+      b4[i] = b;
+      p4[i] = p;
+    }
+    return;
+  }
   for (long long i = threadIdx.x; i < c.count; i += 256) {
-    const float g = c.grad[i] * scale;
-    const float p = c.param[i];
-    const float d = g + c.weight_decay * p;
-    const float b = momentum * c.momentum_buf[i] + d;
+    float p = c.param[i], b = c.momentum_buf[i];
+    sgd1(c.grad[i], p, b, scale, c.weight_decay, c.lr, momentum);
     c.momentum_buf[i] = b;
-    c.param[i] = p - c.lr * b;
+    c.param[i] = p;
   }
 }
 

@@ -61,6 +61,14 @@ def _bs(KS, math):
     return KS == 3 and math != "f32"
 
 
+def _wgrad_1x1_bs(KS, math):
+    """1x1 weight gradients (RPN cls/bbox heads, image-DA conv) under a split-bf16 math run
+    on tlod_conv_wgrad_bs_f32 with KS = 1 (measured 0.135 vs 0.23 ms per step on the f32
+    kernel); their forward / input gradient stay on the f32-MFMA kernels, which beat
+    per-image split-bf16 GEMMs at these sizes (0.26 vs 0.41 ms per step)."""
+    return KS == 1 and math != "f32"
+
+
 def _gemm_conv(KS, math, out_channels):
     """3x3 split-bf16 convs with >= 256 output channels run as an implicit GEMM over
     flattened pixels (tlod_conv3x3_gemm_bs_f32, 256x256 tiles); narrower ones keep the
@@ -214,7 +222,7 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None):
     dw = out if out is not None else torch.empty((Cout, Cin, KS, KS), dtype=torch.float32,
                                                  device=g.device)
     math = wgrad_math() if math is None else math
-    if _bs(KS, math):
+    if _bs(KS, math) or _wgrad_1x1_bs(KS, math):
         nprod = 6 if math == "bf16x6" else 3
         ws = _lib.workspace(L.tlod_conv_wgrad_bs_workspace_bytes(N, Cin, H, W, Cout, KS, nprod),
                             g.device, "wgrad")

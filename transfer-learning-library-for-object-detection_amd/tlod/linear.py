@@ -28,15 +28,17 @@ def linear_math():
     return m
 
 
-def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6"):
-    """c[M][N] = sum_k A(m,k) B(n,k) (+ bias[n]) — see include/tlod.h tlod_gemm_bs_f32."""
+def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6", out=None):
+    """c[M][N] = sum_k A(m,k) B(n,k) (+ bias[n]) — see include/tlod.h tlod_gemm_bs_f32.
+    ``out``: a contiguous (M, N) float32 tensor to write into."""
     _lib.require_cuda(a, b)
     if a.dtype != torch.float32 or b.dtype != torch.float32:
         raise TypeError("tlod gemm computes in fp32 (the reference's dtype)")
     a, b = a.contiguous(), b.contiguous()
     nprod = 6 if math == "bf16x6" else 3
     L = _lib.lib()
-    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device) if out is None else out
+    assert c.is_contiguous() and c.numel() == M * N
     ws = _lib.workspace(L.tlod_gemm_bs_workspace_bytes(M, N, K, a_kcontig, b_kcontig, nprod),
                         a.device, "gemm")
     bias = bias.detach().contiguous() if bias is not None else None
