@@ -118,6 +118,7 @@ def main():
     a = parse()
     from tlod.dist import GradBucketReducer, init_from_env
     from tlod import conv as tconv
+    from tlod.linear import linear_math
     from tlod.detector.train import (SyntheticCityscapes, build_model, make_optimizer,
                                      train_step)
 
@@ -187,7 +188,8 @@ def main():
                                   "kernel_ms_per_step": round(conv_ms / a.steps, 3),
                                   "gflop_per_step": round(conv_f / a.steps / 1e9, 2)},
                      "by_kind": detail},
-        "conv_math": {"3x3 fwd/dgrad": tconv.conv_math(), "wgrad, 1x1": "f32"},
+        "conv_math": {"3x3 fwd/dgrad": tconv.conv_math(), "3x3 and 1x1 wgrad": tconv.wgrad_math(),
+                      "1x1 fwd/dgrad": "f32", "fc6/fc7/DA fc": linear_math()},
         "mean_loss": round(last_loss, 4),
         "cpu_baseline": None,
     }
