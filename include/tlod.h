@@ -357,6 +357,58 @@ int tlod_space_to_depth_f32(const float* x, int B, int C, int H, int W, int scal
 int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int W, int scale, float* dx,
                             tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ Fused losses
+ * One forward launch (single workgroup, fixed-order double accumulation: deterministic)
+ * and one backward launch (writes every gradient element) per loss family.  grad_loss
+ * points to the upstream gradients of the scalar losses on the device (no host sync).
+ *
+ * RPN (lib/model/rpn/rpn.py:89-108): score = RPN_cls_score (B, 2A, H, W) — the
+ *   reference's score_reshape (B, 2, A*H, W) permuted to 2-column rows; labels
+ *   (B, 1, A*H, W) in {-1, 0, 1}; bbox / targets / inside / outside (B, 4A, H, W).
+ *   loss[0] = cross entropy averaged over rows with label != -1 (the reference
+ *   index_selects them with nonzero(), a host sync; count[0] = max(kept, 1) is saved for
+ *   the backward); loss[1] = _smooth_l1_loss(sigma, dim=[1,2,3]) (net_utils.py:72-86).
+ *   dscore (B, 2A, H, W) and dbbox (B, 4A, H, W) are written in full. */
+int tlod_rpn_loss_f32(const float* score, const float* labels, const float* bbox,
+                      const float* targets, const float* inside, const float* outside, int B,
+                      int A, int H, int W, float sigma, float* loss, float* count,
+                      tlod_stream_t stream);
+int tlod_rpn_loss_bwd_f32(const float* score, const float* labels, const float* bbox,
+                          const float* targets, const float* inside, const float* outside,
+                          int B, int A, int H, int W, float sigma, const float* grad_loss,
+                          const float* count, float* dscore, float* dbbox,
+                          tlod_stream_t stream);
+/* RCNN head (lib/DAF/faster_rcnn.py:158-177): cls_score (R, C), bbox_pred (R, 4C) or
+ *   (R, 4) when agnostic, labels int64 (R) in [0, C).  cls_prob = softmax(cls_score);
+ *   bbox_sel (R, 4) = bbox_pred gathered at the label's 4 columns (may be NULL);
+ *   loss[0] = F.cross_entropy, loss[1] = _smooth_l1_loss(sigma, dim=[1]).  Backward:
+ *   dcls (R, C) and dbbox (R, 4C | 4) written in full (zeros off the label's columns). */
+int tlod_rcnn_loss_f32(const float* cls_score, const float* bbox_pred, const long long* labels,
+                       const float* targets, const float* inside, const float* outside, int R,
+                       int C, int agnostic, float sigma, float* cls_prob, float* bbox_sel,
+                       float* loss, tlod_stream_t stream);
+int tlod_rcnn_loss_bwd_f32(const float* cls_prob, const float* bbox_pred,
+                           const long long* labels, const float* targets, const float* inside,
+                           const float* outside, int R, int C, int agnostic, float sigma,
+                           const float* grad_loss, float* dcls, float* dbbox,
+                           tlod_stream_t stream);
+/* DAF domain losses (lib/DAF/faster_rcnn.py:181-220) for the source (s) and target (t)
+ *   domains: image-level logits score (B, 2, H, W), need_backprop (B) float (the image
+ *   label, ImageLabelResizeLayer), instance sigmoid outputs ins (n) with the
+ *   InstanceLabelResizeLayer labels (1, rows [256 i, 256 (i+1)) := need[i]).
+ *   loss[0..2] = source (nll(log_softmax), binary_cross_entropy, MSE-sum consistency
+ *   against softmax(score_s)[:,1].mean()), loss[3..5] = target (same, channel 0);
+ *   cons[2] = the two detached softmax means (saved for the backward). */
+int tlod_da_loss_f32(const float* score_s, const float* score_t, const float* need_s,
+                     const float* need_t, const float* ins_s, const float* ins_t, int Bs,
+                     int Bt, int Hs, int Ws, int Ht, int Wt, int n_s, int n_t, float* loss,
+                     float* cons, tlod_stream_t stream);
+int tlod_da_loss_bwd_f32(const float* score_s, const float* score_t, const float* need_s,
+                         const float* need_t, const float* ins_s, const float* ins_t, int Bs,
+                         int Bt, int Hs, int Ws, int Ht, int Wt, int n_s, int n_t,
+                         const float* grad_loss, const float* cons, float* dscore_s,
+                         float* dscore_t, float* dins_s, float* dins_t, tlod_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,7 +21,8 @@ import torch.nn.functional as F
 from ..config import cfg
 from ..conv import Conv2d
 from ..linear import Linear
-from ..detector.losses import smooth_l1_loss, weighted_loss_sum
+from ..detector.losses import (daf_da_losses, fused_losses, rcnn_losses, smooth_l1_loss,
+                               weighted_loss_sum)
 from ..detector.vgg16 import vgg16_base, vgg16_top
 from ..roi_align import RoIAlignAvg
 from ..roi_pool import _RoIPooling
@@ -73,8 +74,12 @@ class _ImageDA(nn.Module):
         self.Conv1 = Conv2d(dim, 512, 1, bias=False, relu=True)
         self.Conv2 = Conv2d(512, 2, 1, bias=False)
 
+    def score(self, x):
+        """The domain logits alone (the DAF forward discards the label tensor)."""
+        return self.Conv2(self.Conv1(grad_reverse(x)))
+
     def forward(self, x, need_backprop):
-        x = self.Conv2(self.Conv1(grad_reverse(x)))
+        x = self.score(x)
         return x, image_label(x, need_backprop)
 
 
@@ -94,11 +99,15 @@ class _InstanceDA(nn.Module):
         self.dc_drop2 = nn.Dropout(p=0.5)
         self.clssifer = nn.Linear(1024, 1)
 
-    def forward(self, x, need_backprop):
+    def score(self, x):
+        """The sigmoid outputs alone (the DAF forward discards the label tensor)."""
         x = grad_reverse(x)
         x = self.dc_drop1(self.dc_relu1(self.dc_ip1(x)))
         x = self.dc_drop2(self.dc_relu2(self.dc_ip2(x)))
-        x = torch.sigmoid(self.clssifer(x))
+        return torch.sigmoid(self.clssifer(x))
+
+    def forward(self, x, need_backprop):
+        x = self.score(x)
         return x, instance_label(x.shape[0], need_backprop)
 
 
@@ -132,6 +141,9 @@ class _fasterRCNN(nn.Module):
 
     def _rcnn_losses(self, pooled_s, rois_label, rois_target, rois_inside_ws, rois_outside_ws):
         bbox_pred = self.RCNN_bbox_pred(pooled_s)
+        if self.training and fused_losses():
+            return rcnn_losses(self.RCNN_cls_score(pooled_s), bbox_pred, rois_label, rois_target,
+                               rois_inside_ws, rois_outside_ws, self.class_agnostic)
         if self.training and not self.class_agnostic:
             view = bbox_pred.view(bbox_pred.size(0), int(bbox_pred.size(1) / 4), 4)
             bbox_pred = torch.gather(view, 1, rois_label.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
@@ -142,6 +154,8 @@ class _fasterRCNN(nn.Module):
         return cls_prob, bbox_pred, loss_cls, loss_bbox
 
     def _da_losses(self, base_score_s, base_score_t, ins_s, ins_t, need_s, need_t):
+        if fused_losses():
+            return daf_da_losses(base_score_s, base_score_t, ins_s, ins_t, need_s, need_t)
         lab_s = image_label(base_score_s, need_s)
         lab_t = image_label(base_score_t, need_t)
         da_img = F.nll_loss(F.log_softmax(base_score_s, 1), lab_s)
@@ -186,7 +200,7 @@ class _fasterRCNN(nn.Module):
         rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes, im_info,
                                                     num_boxes, rng=self.replay_rng)
         if same:
-            score_img2, _ = self.RCNN_imageDA(base2, need_backprop.new_ones(2))
+            score_img2 = self.RCNN_imageDA.score(base2)
         rois, tgt_rois = pending.join()
         if self.capture is not None:
             self.capture.update(s_rois=rois.detach().clone(), t_rois=tgt_rois.detach().clone())
@@ -217,13 +231,13 @@ class _fasterRCNN(nn.Module):
         # DA heads (faster_rcnn.py:181-220)
         if same:
             base_score, tgt_base_score = score_img2[:1], score_img2[1:]
-            ins2, _ = self.RCNN_instanceDA(feat2, need_backprop.new_ones(1))
+            ins2 = self.RCNN_instanceDA.score(feat2)
             ins_s, ins_t = ins2[:n_s], ins2[n_s:]
         else:
-            base_score, _ = self.RCNN_imageDA(base_feat, need_backprop)
-            tgt_base_score, _ = self.RCNN_imageDA(tgt_base_feat, tgt_need_backprop)
-            ins_s, _ = self.RCNN_instanceDA(pooled_feat, need_backprop)
-            ins_t, _ = self.RCNN_instanceDA(tgt_pooled_feat, tgt_need_backprop)
+            base_score = self.RCNN_imageDA.score(base_feat)
+            tgt_base_score = self.RCNN_imageDA.score(tgt_base_feat)
+            ins_s = self.RCNN_instanceDA.score(pooled_feat)
+            ins_t = self.RCNN_instanceDA.score(tgt_pooled_feat)
         da = self._da_losses(base_score, tgt_base_score, ins_s, ins_t, need_backprop,
                              tgt_need_backprop)
         DA_img_loss_cls, DA_ins_loss_cls, tgt_DA_img_loss_cls, tgt_DA_ins_loss_cls, \

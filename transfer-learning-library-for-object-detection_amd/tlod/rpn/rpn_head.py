@@ -2,7 +2,8 @@
 
 RPN_Conv (3x3 512->512) + ReLU is one fused libtlod conv; cls/bbox 1x1 convs likewise.
 The losses avoid the reference's host syncs (``nonzero`` at :93): cross entropy over
-labels != -1 is computed as a masked mean on device.
+labels != -1 is computed as a masked mean on device, fused with the smooth-L1 box loss into
+one forward and one backward launch (tlod_rpn_loss_f32).
 """
 import torch
 import torch.nn as nn
@@ -10,7 +11,7 @@ import torch.nn.functional as F
 
 from ..config import cfg
 from ..conv import Conv2d
-from ..detector.losses import masked_cross_entropy, smooth_l1_loss
+from ..detector.losses import fused_losses, masked_cross_entropy, rpn_losses, smooth_l1_loss
 from .anchor_target import _AnchorTargetLayer
 from .proposal import _ProposalLayer
 
@@ -51,6 +52,10 @@ class _RPN(nn.Module):
         B = rpn_cls_score.size(0)
         labels, targets, inside, outside = self.RPN_anchor_target(
             (rpn_cls_score.detach(), gt_boxes, im_info, num_boxes), rng=rng)
+        if fused_losses():
+            loss_cls, loss_box = rpn_losses(rpn_cls_score, bbox, labels, targets, inside,
+                                            outside, sigma=3.0)
+            return loss_cls, loss_box, labels
         scores = score_reshape.permute(0, 2, 3, 1).contiguous().view(-1, 2)
         loss_cls = masked_cross_entropy(scores, labels.view(B, -1).view(-1))
         loss_box = smooth_l1_loss(bbox, targets, inside, outside, sigma=3, dim=[1, 2, 3])
