@@ -694,25 +694,28 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 // tap 8-s).
 __global__ void pack_bs_kernel(const float* __restrict__ Wt, unsigned short* __restrict__ P,
                                int rows, int ins, int nchunks, int dgrad) {
+  // one thread per (row o, chunk c, tap slot s): 8 input channels -> one 16-B store per plane
   const size_t rowlen = (size_t)nchunks * kBsKP;
   const size_t plane = (size_t)rows * rowlen;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < plane;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const int o = (int)(i / rowlen);
-    const int k = (int)(i % rowlen);
-    const int e = k % 8, s = (k / 8) % 10, c = k / kBsKP;
-    const int in = c * 8 + e;
-    float v = 0.f;
-    if (in < ins && s < 9)
-      v = dgrad ? Wt[((size_t)in * rows + o) * 9 + (8 - s)] : Wt[((size_t)o * ins + in) * 9 + s];
-    const unsigned u = __float_as_uint(v);
-    const unsigned hb = u & 0xffff0000u;
-    const float r = v - __uint_as_float(hb);
-    const unsigned mb = __float_as_uint(r) & 0xffff0000u;
-    const unsigned lb = __float_as_uint(r - __uint_as_float(mb));
-    P[i] = (unsigned short)(hb >> 16);
-    P[plane + i] = (unsigned short)(mb >> 16);
-    P[2 * plane + i] = (unsigned short)(lb >> 16);
+  const size_t units = (size_t)rows * nchunks * 10;
+  for (size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x; u < units;
+       u += (size_t)gridDim.x * blockDim.x) {
+    const int s = (int)(u % 10);
+    const size_t oc = u / 10;
+    const int c = (int)(oc % nchunks), o = (int)(oc / nchunks);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int in = c * 8 + e;
+      v[e] = 0.f;
+      if (in < ins && s < 9)
+        v[e] = dgrad ? Wt[((size_t)in * rows + o) * 9 + (8 - s)] : Wt[((size_t)o * ins + in) * 9 + s];
+    }
+    u32x4 sp[3];
+    split8<3>(v, sp);
+    const size_t i0 = (size_t)o * rowlen + (size_t)c * kBsKP + s * 8;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(P + pl * plane + i0) = sp[pl];
   }
 }
 
@@ -1227,16 +1230,25 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ Wt, float* __restric
 // residual branch of a bottleneck takes the unscaled gradient).  grid (Cout, N).
 // One workgroup per channel, looping over the N images: db[co] is written (not accumulated),
 // so the caller needs no zero fill, and the sum order is fixed (deterministic).
-__global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restrict__ dY,
-                                                            const float* __restrict__ Y,
-                                                            const float* __restrict__ scale,
-                                                            float* __restrict__ G,
-                                                            float* __restrict__ Graw,
-                                                            float* __restrict__ db, int N,
-                                                            int Cout, int HW) {
+// One workgroup of 1024 threads per channel (the per-channel bias sum stays in one block:
+// deterministic, no second pass); each thread keeps 4 float4 loads of dY and Y in flight,
+// so the kernel streams near the HBM rate even with one workgroup per CU.
+constexpr int kReluThreads = 1024;
+__global__ void __launch_bounds__(kReluThreads) relu_bwd_bias_kernel(
+    const float* __restrict__ dY, const float* __restrict__ Y, const float* __restrict__ scale,
+    float* __restrict__ G, float* __restrict__ Graw, float* __restrict__ db, int N, int Cout,
+    int HW) {
   const int co = blockIdx.x;
   const float sc = scale ? scale[co] : 1.f;
+  const bool write_g = G != dY || Y != nullptr || scale != nullptr;
   float s = 0.f;
+  auto apply = [&](float4 d, float4 y, bool has_y) {
+    if (has_y) {
+      d.x = y.x > 0.f ? d.x : 0.f; d.y = y.y > 0.f ? d.y : 0.f;
+      d.z = y.z > 0.f ? d.z : 0.f; d.w = y.w > 0.f ? d.w : 0.f;
+    }
+    return d;
+  };
   const bool vec = (HW % 4) == 0;
   for (int n = 0; n < N; ++n) {
     const size_t base = ((size_t)n * Cout + co) * HW;
@@ -1245,20 +1257,34 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
       const float4* y4 = Y ? reinterpret_cast<const float4*>(Y + base) : nullptr;
       float4* g4 = reinterpret_cast<float4*>(G + base);
       float4* r4 = Graw ? reinterpret_cast<float4*>(Graw + base) : nullptr;
-      for (int i = threadIdx.x; i < HW / 4; i += 256) {
-        float4 d = d4[i];
+      const int n4 = HW / 4;
+      constexpr int U = 4;
+      int i = threadIdx.x;
+      for (; i + (U - 1) * kReluThreads < n4; i += U * kReluThreads) {
+        float4 d[U], y[U] = {};
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = d4[i + u * kReluThreads];
         if (y4) {
-          const float4 y = y4[i];
-          d.x = y.x > 0.f ? d.x : 0.f; d.y = y.y > 0.f ? d.y : 0.f;
-          d.z = y.z > 0.f ? d.z : 0.f; d.w = y.w > 0.f ? d.w : 0.f;
+#pragma unroll
+          for (int u = 0; u < U; ++u) y[u] = y4[i + u * kReluThreads];
         }
-        if (r4) r4[i] = d;
-        s += (d.x + d.y) + (d.z + d.w);
-        if (scale) { d.x *= sc; d.y *= sc; d.z *= sc; d.w *= sc; }
-        if (G != dY || y4 || scale) g4[i] = d;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float4 v = apply(d[u], y[u], y4 != nullptr);
+          if (r4) r4[i + u * kReluThreads] = v;
+          s += (v.x + v.y) + (v.z + v.w);
+          if (write_g)
+            g4[i + u * kReluThreads] = scale ? make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc) : v;
+        }
+      }
+      for (; i < n4; i += kReluThreads) {
+        const float4 v = apply(d4[i], y4 ? y4[i] : make_float4(0.f, 0.f, 0.f, 0.f), y4 != nullptr);
+        if (r4) r4[i] = v;
+        s += (v.x + v.y) + (v.z + v.w);
+        if (write_g) g4[i] = scale ? make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc) : v;
       }
     } else {
-      for (int i = threadIdx.x; i < HW; i += 256) {
+      for (int i = threadIdx.x; i < HW; i += kReluThreads) {
         float d = dY[base + i];
         if (Y) d = Y[base + i] > 0.f ? d : 0.f;
         if (Graw) Graw[base + i] = d;
@@ -1269,10 +1295,14 @@ __global__ void __launch_bounds__(256) relu_bwd_bias_kernel(const float* __restr
   }
   if (!db) return;
   for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-  __shared__ float ws[4];
+  __shared__ float ws[kReluThreads / 64];
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) db[co] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kReluThreads / 64; ++w) t += ws[w];
+    db[co] = t;
+  }
 }
 
 // ======================================================================= launchers
@@ -1766,8 +1796,8 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
 extern "C" int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db,
                                       int N, int C, int HW, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0, "bad shape");
-  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, y,
-                     nullptr, g, nullptr, db, N, C, HW);
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C), dim3(kReluThreads), 0, (hipStream_t)stream,
+                     dy, y, nullptr, g, nullptr, db, N, C, HW);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }
@@ -1777,8 +1807,8 @@ extern "C" int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float
                                     tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && C > 0 && HW > 0 && dy && g, "bad arguments");
   TLOD_CHECK_ARG(g_raw != g || g_raw == nullptr, "g_raw must not alias g");
-  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, y,
-                     scale, g, g_raw, db, N, C, HW);
+  hipLaunchKernelGGL(relu_bwd_bias_kernel, dim3(C), dim3(kReluThreads), 0, (hipStream_t)stream,
+                     dy, y, scale, g, g_raw, db, N, C, HW);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }
@@ -1794,7 +1824,7 @@ extern "C" int tlod_conv_pack_bs(const float* weight, int Cout, int Cin, int KS,
   TLOD_CHECK_ARG(Cout > 0 && Cin > 0 && weight && packed, "bad arguments");
   TLOD_CHECK_ARG(KS == 3, "split-bf16 conv: 3x3 only");
   const int rows = dgrad ? Cin : Cout, ins = dgrad ? Cout : Cin;
-  const size_t plane = (size_t)rows * div_up(ins, 8) * kBsKP;
+  const size_t plane = (size_t)rows * div_up(ins, 8) * 10;  // threads: (row, chunk, tap slot)
   hipLaunchKernelGGL(pack_bs_kernel, dim3((unsigned)std::min<size_t>((plane + 255) / 256, 4096)),
                      dim3(256), 0, (hipStream_t)stream, weight, (unsigned short*)packed, rows, ins,
                      div_up(ins, 8), dgrad);

@@ -41,47 +41,81 @@ __global__ void maxpool2x2_kernel(const float* __restrict__ x, int NC, int H, in
   }
 }
 
-// One workgroup per channel c looping over the N images (db written, deterministic order);
-// each thread handles one pooled column pair of a row pair per iteration.
-__global__ void __launch_bounds__(256) maxpool2x2_relu_bwd_kernel(
+// One workgroup of 1024 threads per channel c looping over the N images (db written,
+// deterministic order); each thread handles two windows per iteration, reading the window
+// rows as float2 pairs when W is even (8-byte aligned rows), so two loads of y, one of dp
+// and two stores of g per window are in flight together.
+constexpr int kPoolThreads = 1024;
+__global__ void __launch_bounds__(kPoolThreads) maxpool2x2_relu_bwd_kernel(
     const float* __restrict__ dp, const float* __restrict__ y, int N, int C, int H, int W,
     float* __restrict__ g, float* __restrict__ db) {
   const int c = blockIdx.x;
   const int Hp = H / 2, Wp = W / 2;
+  const int nw = Hp * Wp;
   float s = 0.f;
+  auto window = [&](const float a, const float b, const float cc, const float d, float gv,
+                    float (&out)[4]) {
+    float m;
+    const int k = window_argmax(a, b, cc, d, m);
+    const float v[4] = {a, b, cc, d};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = (e == k && v[e] > 0.f) ? gv : 0.f;
+    s += (out[0] + out[1]) + (out[2] + out[3]);
+  };
   for (int n = 0; n < N; ++n) {
     const size_t base = ((size_t)n * C + c) * H * W;
     const size_t pbase = ((size_t)n * C + c) * Hp * Wp;
-    // windows
-    for (int o = threadIdx.x; o < Hp * Wp; o += 256) {
-      const int i = o / Wp, j = o - i * Wp;
-      const size_t i00 = base + (size_t)(2 * i) * W + 2 * j;
-      const float a = y[i00], b = y[i00 + 1], cc = y[i00 + W], d = y[i00 + W + 1];
-      float m;
-      const int k = window_argmax(a, b, cc, d, m);
-      const float gv = dp[pbase + o];
-      const float v[4] = {a, b, cc, d};
-      float out[4];
+    if ((W & 1) == 0) {
+      for (int o0 = threadIdx.x; o0 < nw; o0 += 2 * kPoolThreads) {
+        float2 r0[2], r1[2];
+        float gv[2];
+        int idx[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) out[e] = (e == k && v[e] > 0.f) ? gv : 0.f;
-      g[i00] = out[0];
-      g[i00 + 1] = out[1];
-      g[i00 + W] = out[2];
-      g[i00 + W + 1] = out[3];
-      s += (out[0] + out[1]) + (out[2] + out[3]);
+        for (int u = 0; u < 2; ++u) {
+          const int o = min(o0 + u * kPoolThreads, nw - 1);
+          const int i = o / Wp, jj = o - i * Wp;
+          idx[u] = (2 * i) * W + 2 * jj;
+          r0[u] = *reinterpret_cast<const float2*>(y + base + idx[u]);
+          r1[u] = *reinterpret_cast<const float2*>(y + base + idx[u] + W);
+          gv[u] = dp[pbase + o];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (o0 + u * kPoolThreads >= nw) continue;
+          float out[4];
+          window(r0[u].x, r0[u].y, r1[u].x, r1[u].y, gv[u], out);
+          *reinterpret_cast<float2*>(g + base + idx[u]) = make_float2(out[0], out[1]);
+          *reinterpret_cast<float2*>(g + base + idx[u] + W) = make_float2(out[2], out[3]);
+        }
+      }
+    } else {
+      for (int o = threadIdx.x; o < nw; o += kPoolThreads) {
+        const int i = o / Wp, j = o - i * Wp;
+        const size_t i00 = base + (size_t)(2 * i) * W + 2 * j;
+        float out[4];
+        window(y[i00], y[i00 + 1], y[i00 + W], y[i00 + W + 1], dp[pbase + o], out);
+        g[i00] = out[0];
+        g[i00 + 1] = out[1];
+        g[i00 + W] = out[2];
+        g[i00 + W + 1] = out[3];
+      }
     }
     // floor mode: the odd last column / row get no gradient
     if (W & 1)
-      for (int h = threadIdx.x; h < H; h += 256) g[base + (size_t)h * W + W - 1] = 0.f;
+      for (int h = threadIdx.x; h < H; h += kPoolThreads) g[base + (size_t)h * W + W - 1] = 0.f;
     if (H & 1)
-      for (int w = threadIdx.x; w < W; w += 256) g[base + (size_t)(H - 1) * W + w] = 0.f;
+      for (int w = threadIdx.x; w < W; w += kPoolThreads) g[base + (size_t)(H - 1) * W + w] = 0.f;
   }
   if (!db) return;
   for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-  __shared__ float ws[4];
+  __shared__ float ws[kPoolThreads / 64];
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) db[c] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kPoolThreads / 64; ++w) t += ws[w];
+    db[c] = t;
+  }
 }
 
 }  // namespace tlod
@@ -101,8 +135,8 @@ extern "C" int tlod_maxpool2x2_f32(const float* x, int N, int C, int H, int W, f
 extern "C" int tlod_maxpool2x2_relu_bwd_f32(const float* dp, const float* y, int N, int C, int H,
                                             int W, float* g, float* db, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && C > 0 && H >= 2 && W >= 2 && dp && y && g, "bad arguments");
-  hipLaunchKernelGGL(maxpool2x2_relu_bwd_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dp, y,
-                     N, C, H, W, g, db);
+  hipLaunchKernelGGL(maxpool2x2_relu_bwd_kernel, dim3(C), dim3(kPoolThreads), 0,
+                     (hipStream_t)stream, dp, y, N, C, H, W, g, db);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

@@ -100,7 +100,23 @@ def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind):
 
 
 def pack_bs(weight, dgrad):
-    """Pre-split bf16 planes of a 3x3 weight for the split-bf16 fwd (dgrad=0) / dgrad (1)."""
+    """Pre-split bf16 planes of a 3x3 weight for the split-bf16 fwd (dgrad=0) / dgrad (1).
+    Frozen weights (requires_grad False: conv1/conv2 of VGG16, the fixed ResNet blocks) are
+    packed once per (storage, version), cached on the tensor itself — an in-place load bumps
+    the version; trainable weights are repacked every call (the fused SGD writes them
+    without a version bump).  One cached pack per tensor (a frozen weight is packed for the
+    forward only)."""
+    if not weight.requires_grad:
+        cache = getattr(weight, "_tlod_packs", None)  # lives and dies with the tensor
+        key = (weight.data_ptr(), weight._version, bool(dgrad))
+        if cache is None or cache[0] != key:
+            cache = (key, _pack_bs(weight, dgrad))
+            weight._tlod_packs = cache
+        return cache[1]
+    return _pack_bs(weight, dgrad)
+
+
+def _pack_bs(weight, dgrad):
     Cout, Cin, KS, _ = weight.shape
     L = _lib.lib()
     p = torch.empty(L.tlod_conv_pack_bs_bytes(Cout, Cin, KS, int(dgrad)), dtype=torch.uint8,
