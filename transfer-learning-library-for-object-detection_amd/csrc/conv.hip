@@ -44,6 +44,9 @@ namespace tlod {
 #endif
 // Split-bf16 forward: pair the 9 taps across consecutive input-channel chunks instead of
 // padding each chunk to 10 tap slots (0 = pad, for A/B).
+#ifndef TLOD_WG_SWZ
+#define TLOD_WG_SWZ 1
+#endif
 #ifndef TLOD_TAP_PAIRING
 #define TLOD_TAP_PAIRING 1
 #endif
@@ -941,7 +944,10 @@ struct WgBsCfg {
   static constexpr int BM = WM * MI * 32;
   static constexpr int BN = WN * NJ * 32;
   static constexpr int TK = 16;                    // pixels per chunk (one k-step)
-  static constexpr int PITCH = 48;                 // bytes per row per plane (32 used)
+  // bytes per row per plane: 32 (dense) with the two 16-B halves swapped on rows with bit 3
+  // set — conflict-free for both the staging ds_write_b64 (16-lane groups = 4 rows) and the
+  // fragment ds_read_b128; TLOD_WG_SWZ=0: the padded 48-B pitch (2-way write conflicts)
+  static constexpr int PITCH = TLOD_WG_SWZ ? 32 : 48;
   static constexpr int A_PLANE = BM * PITCH;
   static constexpr int B_PLANE = BN * PITCH;
   static constexpr int BUF = NPL * (A_PLANE + B_PLANE);
@@ -951,6 +957,11 @@ struct WgBsCfg {
   static_assert(BM % ROWS_PER_IT == 0 && BN % ROWS_PER_IT == 0, "staging");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
+
+// byte offset of pixel px (a multiple of 4) of a staged row inside the row (see WgBsCfg)
+__device__ __forceinline__ int wg_slot(int row, int px) {
+  return TLOD_WG_SWZ ? (((px >> 3) ^ ((row >> 3) & 1)) << 4) + ((px & 4) << 1) : 2 * px;
+}
 
 template <int WM, int WN, int MI, int NJ, int KS, int NP>
 __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kernel(
@@ -988,7 +999,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
   for (int i = 0; i < C::A_IT; ++i) {
     const int row = (tid >> 2) + i * C::ROWS_PER_IT;
     a_off[i] = m0 + row < Cout ? (m0 + row) * P + s4 : -1;  // -1: row past Cout
-    a_lds[i] = row * C::PITCH + 2 * s4;
+    a_lds[i] = row * C::PITCH + wg_slot(row, s4);
   }
   int b_off[C::B_IT], b_lds[C::B_IT], b_dh[C::B_IT], b_dw[C::B_IT];
 #pragma unroll
@@ -1000,7 +1011,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
     b_dh[i] = ok ? s / KS - KS / 2 : -(1 << 20);  // dead column: never in the map
     b_dw[i] = s % KS - KS / 2;
     b_off[i] = ok ? ci * P + b_dh[i] * W + b_dw[i] + s4 : s4;
-    b_lds[i] = C::NPL * C::A_PLANE + cl * C::PITCH + 2 * s4;
+    b_lds[i] = C::NPL * C::A_PLANE + cl * C::PITCH + wg_slot(cl, s4);
   }
   f32x4v ra[C::A_IT], rb[C::B_IT];
   unsigned a_mask = 0, b_mask[C::B_IT];
@@ -1086,8 +1097,8 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int a_rd = (wm * MI * 32 + l32) * C::PITCH + 16 * khalf;
-  const int b_rd = C::NPL * C::A_PLANE + (wn * NJ * 32 + l32) * C::PITCH + 16 * khalf;
+  const int a_rd = (wm * MI * 32 + l32) * C::PITCH + wg_slot(l32, 8 * khalf);
+  const int b_rd = C::NPL * C::A_PLANE + (wn * NJ * 32 + l32) * C::PITCH + wg_slot(l32, 8 * khalf);
   if (c_begin < c_end) {
     load_chunk(c_begin);
     store_chunk(smem);
