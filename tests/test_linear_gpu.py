@@ -56,6 +56,7 @@ def test_gemm_split_k_deterministic():
 
 
 @pytest.mark.parametrize("R,I,O", [(556, 25088, 4096), (556, 4096, 4096), (556, 4096, 1024),
+                                   (256, 4096, 9), (256, 4096, 36), (556, 1024, 1), (556, 2048, 9),
                                    (256, 4105, 1024), (3, 100, 20)])
 def test_linear_fwd_bwd(R, I, O):
     """tlod.linear.Linear forward, input / weight / bias gradients vs nn.Linear in fp64."""
