@@ -368,29 +368,33 @@ int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int W, int sca
  *   loss[0] = cross entropy averaged over rows with label != -1 (the reference
  *   index_selects them with nonzero(), a host sync; count[0] = max(kept, 1) is saved for
  *   the backward); loss[1] = _smooth_l1_loss(sigma, dim=[1,2,3]) (net_utils.py:72-86).
- *   dscore (B, 2A, H, W) and dbbox (B, 4A, H, W) are written in full. */
+ *   Backward: score / bbox may hold B_total >= B images of which the first B are the
+ *   loss's; dscore (B_total, 2A, H, W) and dbbox (B_total, 4A, H, W) are written in full
+ *   (zero past image B). */
 int tlod_rpn_loss_f32(const float* score, const float* labels, const float* bbox,
                       const float* targets, const float* inside, const float* outside, int B,
                       int A, int H, int W, float sigma, float* loss, float* count,
                       tlod_stream_t stream);
 int tlod_rpn_loss_bwd_f32(const float* score, const float* labels, const float* bbox,
                           const float* targets, const float* inside, const float* outside,
-                          int B, int A, int H, int W, float sigma, const float* grad_loss,
-                          const float* count, float* dscore, float* dbbox,
-                          tlod_stream_t stream);
+                          int B, int B_total, int A, int H, int W, float sigma,
+                          const float* grad_loss, const float* count, float* dscore,
+                          float* dbbox, tlod_stream_t stream);
 /* RCNN head (lib/DAF/faster_rcnn.py:158-177): cls_score (R, C), bbox_pred (R, 4C) or
  *   (R, 4) when agnostic, labels int64 (R) in [0, C).  cls_prob = softmax(cls_score);
  *   bbox_sel (R, 4) = bbox_pred gathered at the label's 4 columns (may be NULL);
  *   loss[0] = F.cross_entropy, loss[1] = _smooth_l1_loss(sigma, dim=[1]).  Backward:
- *   dcls (R, C) and dbbox (R, 4C | 4) written in full (zeros off the label's columns). */
+ *   cls_score / bbox_pred may hold R_total >= R rows of which the first R are the loss's;
+ *   dcls (R_total, C) and dbbox (R_total, 4C | 4) are written in full (zeros off the
+ *   label's columns and past row R). */
 int tlod_rcnn_loss_f32(const float* cls_score, const float* bbox_pred, const long long* labels,
                        const float* targets, const float* inside, const float* outside, int R,
                        int C, int agnostic, float sigma, float* cls_prob, float* bbox_sel,
                        float* loss, tlod_stream_t stream);
 int tlod_rcnn_loss_bwd_f32(const float* cls_prob, const float* bbox_pred,
                            const long long* labels, const float* targets, const float* inside,
-                           const float* outside, int R, int C, int agnostic, float sigma,
-                           const float* grad_loss, float* dcls, float* dbbox,
+                           const float* outside, int R, int R_total, int C, int agnostic,
+                           float sigma, const float* grad_loss, float* dcls, float* dbbox,
                            tlod_stream_t stream);
 /* DAF domain losses (lib/DAF/faster_rcnn.py:181-220) for the source (s) and target (t)
  *   domains: image-level logits score (B, 2, H, W), need_backprop (B) float (the image

@@ -139,3 +139,62 @@ def test_da_losses(Bs, Bt, Hs, Ws, Ht, Wt, n_s, n_t):
             assert a.grad is None or a.grad.numel() == 0 or torch.count_nonzero(a.grad) == 0
         else:
             close(a.grad, b.grad)
+
+
+def test_rpn_loss_partial_batch():
+    """Loss over the first image of a 2-image head batch: the gradient of the second image
+    is zero and the first matches the single-image loss."""
+    from tlod.detector.losses import rpn_losses
+    score, bbox, lab, tgt, inside, outside = rpn_inputs(1, 12, 37, 75, 11)
+    g = torch.Generator().manual_seed(12)
+    score2 = torch.cat([score, torch.randn(score.shape, generator=g).to(dev)], 0)
+    bbox2 = torch.cat([bbox, torch.randn(bbox.shape, generator=g).to(dev)], 0)
+    s2, b2 = score2.clone().requires_grad_(True), bbox2.clone().requires_grad_(True)
+    lc2, lb2 = rpn_losses(s2, b2, lab, tgt, inside, outside)
+    (lc2 + lb2).backward()
+    s1, b1 = score.clone().requires_grad_(True), bbox.clone().requires_grad_(True)
+    lc1, lb1 = rpn_losses(s1, b1, lab, tgt, inside, outside)
+    (lc1 + lb1).backward()
+    assert torch.equal(lc1, lc2) and torch.equal(lb1, lb2)
+    assert torch.equal(s2.grad[:1], s1.grad) and torch.equal(b2.grad[:1], b1.grad)
+    assert torch.count_nonzero(s2.grad[1:]) == 0 and torch.count_nonzero(b2.grad[1:]) == 0
+
+
+def test_rcnn_loss_partial_rows():
+    from tlod.detector.losses import rcnn_losses
+    g = torch.Generator().manual_seed(3)
+    R, Rt, C = 256, 556, 9
+    cls = torch.randn(Rt, C, generator=g).to(dev)
+    box = torch.randn(Rt, 4 * C, generator=g).to(dev)
+    lab = torch.randint(0, C, (R,), generator=g).to(dev)
+    tgt = torch.randn(R, 4, generator=g).to(dev)
+    w = (lab > 0).float()[:, None].expand(R, 4).contiguous()
+    c2, b2 = cls.clone().requires_grad_(True), box.clone().requires_grad_(True)
+    p2, s2, lc2, lb2 = rcnn_losses(c2, b2, lab, tgt, w, w)
+    (lc2 + 2 * lb2).backward()
+    c1, b1 = cls[:R].clone().requires_grad_(True), box[:R].clone().requires_grad_(True)
+    p1, s1, lc1, lb1 = rcnn_losses(c1, b1, lab, tgt, w, w)
+    (lc1 + 2 * lb1).backward()
+    assert torch.equal(p1, p2) and torch.equal(s1, s2)
+    assert torch.equal(lc1, lc2) and torch.equal(lb1, lb2)
+    assert torch.equal(c2.grad[:R], c1.grad) and torch.equal(b2.grad[:R], b1.grad)
+    assert torch.count_nonzero(c2.grad[R:]) == 0 and torch.count_nonzero(b2.grad[R:]) == 0
+
+
+def test_da_losses_packed_matches_split():
+    from tlod.detector.losses import daf_da_losses, daf_da_losses_packed
+    g = torch.Generator().manual_seed(21)
+    sc = (torch.randn(2, 2, 37, 75, generator=g) * 2).to(dev)
+    ins = torch.rand(556, 1, generator=g).to(dev)
+    need_s, need_t = torch.ones(1, device=dev), torch.zeros(1, device=dev)
+    w = torch.tensor([1.0, 0.5, 2.0, 0.25, 3.0, 0.125], device=dev)
+    a_sc, a_in = sc.clone().requires_grad_(True), ins.clone().requires_grad_(True)
+    got = daf_da_losses_packed(a_sc, a_in, 1, 256, need_s, need_t)
+    (torch.stack(got) @ w).backward()
+    xs = [t.clone().requires_grad_(True) for t in (sc[:1], sc[1:], ins[:256], ins[256:])]
+    ref = daf_da_losses(*xs, need_s, need_t)
+    (torch.stack(ref) @ w).backward()
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    assert torch.equal(a_sc.grad, torch.cat([xs[0].grad, xs[1].grad], 0))
+    assert torch.equal(a_in.grad, torch.cat([xs[2].grad, xs[3].grad], 0))

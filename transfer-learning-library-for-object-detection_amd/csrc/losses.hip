@@ -99,18 +99,19 @@ __global__ void __launch_bounds__(256)
 rpn_loss_bwd_kernel(const float* __restrict__ score, const float* __restrict__ labels,
                     const float* __restrict__ bbox, const float* __restrict__ tgt,
                     const float* __restrict__ inw, const float* __restrict__ outw, int B,
-                    int AHW, float s2, const float* __restrict__ gloss,
+                    int B_total, int AHW, float s2, const float* __restrict__ gloss,
                     const float* __restrict__ count, float* __restrict__ dscore,
                     float* __restrict__ dbbox) {
-  const long long rows = (long long)B * AHW;
-  const long long ne = rows * 4;
+  // images B .. B_total-1 of score / bbox take no part in the loss: zero gradient
+  const long long rows = (long long)B_total * AHW, lrows = (long long)B * AHW;
+  const long long ne = rows * 4, lne = lrows * 4;
   const float gc = gloss[0] / count[0], gb = gloss[1] / B;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < rows + ne;
        i += (long long)gridDim.x * blockDim.x) {
     if (i < rows) {
       const long long b = i / AHW, q = i - b * AHW;
       const long long i0 = b * 2 * AHW + q, i1 = i0 + AHW;
-      const float lab = labels[i];
+      const float lab = i < lrows ? labels[i] : -1.f;
       float d0 = 0.f, d1 = 0.f;
       if (lab != -1.f) {
         const float s0 = score[i0], s1 = score[i1];
@@ -124,8 +125,8 @@ rpn_loss_bwd_kernel(const float* __restrict__ score, const float* __restrict__ l
       dscore[i1] = d1;
     } else {
       const long long e = i - rows;
-      float dp;
-      smooth_l1(bbox[e], tgt[e], inw[e], outw[e], s2, &dp);
+      float dp = 0.f;
+      if (e < lne) smooth_l1(bbox[e], tgt[e], inw[e], outw[e], s2, &dp);
       dbbox[e] = gb * dp;
     }
   }
@@ -170,20 +171,30 @@ __global__ void __launch_bounds__(256)
 rcnn_loss_bwd_kernel(const float* __restrict__ prob, const float* __restrict__ box,
                      const long long* __restrict__ labels, const float* __restrict__ tgt,
                      const float* __restrict__ inw, const float* __restrict__ outw, int R,
-                     int C, int agnostic, float s2, const float* __restrict__ gloss,
-                     float* __restrict__ dcls, float* __restrict__ dbox) {
+                     int R_total, int C, int agnostic, float s2,
+                     const float* __restrict__ gloss, float* __restrict__ dcls,
+                     float* __restrict__ dbox) {
+  // rows R .. R_total-1 of cls_score / bbox_pred take no part in the loss: zero gradient
   const float gc = gloss[0] / R, gb = gloss[1] / R;
   const int BW = agnostic ? 4 : 4 * C;
-  const long long nc = (long long)R * C, nb = (long long)R * BW;
+  const long long nc = (long long)R_total * C, nb = (long long)R_total * BW;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nc + nb;
        i += (long long)gridDim.x * blockDim.x) {
     if (i < nc) {
       const int r = (int)(i / C), c = (int)(i - (long long)r * C);
+      if (r >= R) {
+        dcls[i] = 0.f;
+        continue;
+      }
       const long long l = labels[r];
       dcls[i] = gc * (prob[i] - ((l < 0 || l >= C ? 0 : l) == c ? 1.f : 0.f));
     } else {
       const long long e = i - nc;
       const int r = (int)(e / BW), j = (int)(e - (long long)r * BW);
+      if (r >= R) {
+        dbox[e] = 0.f;
+        continue;
+      }
       const long long l = labels[r];
       const int lab = agnostic || l < 0 || l >= C ? 0 : (int)l;
       float d = 0.f;
@@ -310,16 +321,17 @@ int tlod_rpn_loss_f32(const float* score, const float* labels, const float* bbox
 
 int tlod_rpn_loss_bwd_f32(const float* score, const float* labels, const float* bbox,
                           const float* targets, const float* inside, const float* outside,
-                          int B, int A, int H, int W, float sigma, const float* grad_loss,
-                          const float* count, float* dscore, float* dbbox,
-                          tlod_stream_t stream) {
+                          int B, int B_total, int A, int H, int W, float sigma,
+                          const float* grad_loss, const float* count, float* dscore,
+                          float* dbbox, tlod_stream_t stream) {
   TLOD_CHECK_ARG(score && labels && bbox && targets && inside && outside && grad_loss &&
                  count && dscore && dbbox, "null pointer");
-  TLOD_CHECK_ARG(B > 0 && A > 0 && H > 0 && W > 0 && sigma > 0.f, "bad shape / sigma");
-  const long long rows = (long long)B * A * H * W;
+  TLOD_CHECK_ARG(B > 0 && B_total >= B && A > 0 && H > 0 && W > 0 && sigma > 0.f,
+                 "bad shape / sigma");
+  const long long rows = (long long)B_total * A * H * W;
   rpn_loss_bwd_kernel<<<grid_for(rows * 5), 256, 0, (hipStream_t)stream>>>(
-      score, labels, bbox, targets, inside, outside, B, A * H * W, sigma * sigma, grad_loss,
-      count, dscore, dbbox);
+      score, labels, bbox, targets, inside, outside, B, B_total, A * H * W, sigma * sigma,
+      grad_loss, count, dscore, dbbox);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }
@@ -340,16 +352,16 @@ int tlod_rcnn_loss_f32(const float* cls_score, const float* bbox_pred, const lon
 
 int tlod_rcnn_loss_bwd_f32(const float* cls_prob, const float* bbox_pred,
                            const long long* labels, const float* targets, const float* inside,
-                           const float* outside, int R, int C, int agnostic, float sigma,
-                           const float* grad_loss, float* dcls, float* dbbox,
+                           const float* outside, int R, int R_total, int C, int agnostic,
+                           float sigma, const float* grad_loss, float* dcls, float* dbbox,
                            tlod_stream_t stream) {
   TLOD_CHECK_ARG(cls_prob && bbox_pred && labels && targets && inside && outside &&
                  grad_loss && dcls && dbbox, "null pointer");
-  TLOD_CHECK_ARG(R > 0 && C > 0 && sigma > 0.f, "bad shape / sigma");
-  const long long n = (long long)R * C + (long long)R * (agnostic ? 4 : 4 * C);
+  TLOD_CHECK_ARG(R > 0 && R_total >= R && C > 0 && sigma > 0.f, "bad shape / sigma");
+  const long long n = (long long)R_total * C + (long long)R_total * (agnostic ? 4 : 4 * C);
   rcnn_loss_bwd_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(
-      cls_prob, bbox_pred, labels, targets, inside, outside, R, C, agnostic, sigma * sigma,
-      grad_loss, dcls, dbbox);
+      cls_prob, bbox_pred, labels, targets, inside, outside, R, R_total, C, agnostic,
+      sigma * sigma, grad_loss, dcls, dbbox);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

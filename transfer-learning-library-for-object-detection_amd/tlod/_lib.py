@@ -116,11 +116,11 @@ SIGNATURES = {
     "tlod_depth_to_space_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_rpn_loss_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, P, P,
                                   P]),
-    "tlod_rpn_loss_bwd_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, P,
-                                      P, P, P, P]),
+    "tlod_rpn_loss_bwd_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                                      c_float, P, P, P, P, P]),
     "tlod_rcnn_loss_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P, P, P, P]),
-    "tlod_rcnn_loss_bwd_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P, P, P,
-                                       P]),
+    "tlod_rcnn_loss_bwd_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, P,
+                                       P, P, P]),
     "tlod_da_loss_f32": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, P]),
     "tlod_da_loss_bwd_f32": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, P, P, P, P, P]),
 }

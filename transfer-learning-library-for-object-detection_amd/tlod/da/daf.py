@@ -21,8 +21,8 @@ import torch.nn.functional as F
 from ..config import cfg
 from ..conv import Conv2d
 from ..linear import Linear
-from ..detector.losses import (daf_da_losses, fused_losses, rcnn_losses, smooth_l1_loss,
-                               weighted_loss_sum)
+from ..detector.losses import (daf_da_losses, daf_da_losses_packed, fused_losses, rcnn_losses,
+                               smooth_l1_loss, weighted_loss_sum)
 from ..detector.vgg16 import vgg16_base, vgg16_top
 from ..roi_align import RoIAlignAvg
 from ..roi_pool import _RoIPooling
@@ -140,10 +140,15 @@ class _fasterRCNN(nn.Module):
         raise NotImplementedError("POOLING_MODE 'crop' is out of scope (configs use 'align')")
 
     def _rcnn_losses(self, pooled_s, rois_label, rois_target, rois_inside_ws, rois_outside_ws):
+        """Head outputs and losses of the first rois_label.numel() rows of ``pooled_s``
+        (the source RoIs; the batched pass appends the target RoIs, whose head outputs
+        are unused)."""
         bbox_pred = self.RCNN_bbox_pred(pooled_s)
         if self.training and fused_losses():
             return rcnn_losses(self.RCNN_cls_score(pooled_s), bbox_pred, rois_label, rois_target,
                                rois_inside_ws, rois_outside_ws, self.class_agnostic)
+        n_s = rois_label.numel()
+        pooled_s, bbox_pred = pooled_s[:n_s], bbox_pred[:n_s]
         if self.training and not self.class_agnostic:
             view = bbox_pred.view(bbox_pred.size(0), int(bbox_pred.size(1) / 4), 4)
             bbox_pred = torch.gather(view, 1, rois_label.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
@@ -197,8 +202,12 @@ class _fasterRCNN(nn.Module):
         pending = proposals_on_side_streams(rpn.RPN_proposal, [
             (s_prob.detach(), s_bbox.detach(), im_info, "TRAIN"),
             (t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST")])
-        rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes, im_info,
-                                                    num_boxes, rng=self.replay_rng)
+        if same:  # the source image's losses over the batched head outputs
+            rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(score2, score_r2, bbox2, gt_boxes, im_info,
+                                                        num_boxes, rng=self.replay_rng, n_images=1)
+        else:
+            rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes,
+                                                        im_info, num_boxes, rng=self.replay_rng)
         if same:
             score_img2 = self.RCNN_imageDA.score(base2)
         rois, tgt_rois = pending.join()
@@ -224,22 +233,27 @@ class _fasterRCNN(nn.Module):
             tgt_pooled_feat = self._head_to_tail(self._pool(tgt_base_feat, tgt_rois.view(-1, 5)))
 
         cls_prob, bbox_pred, RCNN_loss_cls, RCNN_loss_bbox = self._rcnn_losses(
-            pooled_feat, rois_label, rois_target, rois_inside_ws, rois_outside_ws)
+            feat2 if same else pooled_feat, rois_label, rois_target, rois_inside_ws,
+            rois_outside_ws)
         cls_prob = cls_prob.view(batch_size, n_s, -1)
         bbox_pred = bbox_pred.view(batch_size, n_s, -1)
 
         # DA heads (faster_rcnn.py:181-220)
         if same:
-            base_score, tgt_base_score = score_img2[:1], score_img2[1:]
             ins2 = self.RCNN_instanceDA.score(feat2)
-            ins_s, ins_t = ins2[:n_s], ins2[n_s:]
+            if fused_losses():
+                da = daf_da_losses_packed(score_img2, ins2, 1, n_s, need_backprop,
+                                          tgt_need_backprop)
+            else:
+                da = self._da_losses(score_img2[:1], score_img2[1:], ins2[:n_s], ins2[n_s:],
+                                     need_backprop, tgt_need_backprop)
         else:
             base_score = self.RCNN_imageDA.score(base_feat)
             tgt_base_score = self.RCNN_imageDA.score(tgt_base_feat)
             ins_s = self.RCNN_instanceDA.score(pooled_feat)
             ins_t = self.RCNN_instanceDA.score(tgt_pooled_feat)
-        da = self._da_losses(base_score, tgt_base_score, ins_s, ins_t, need_backprop,
-                             tgt_need_backprop)
+            da = self._da_losses(base_score, tgt_base_score, ins_s, ins_t, need_backprop,
+                                 tgt_need_backprop)
         DA_img_loss_cls, DA_ins_loss_cls, tgt_DA_img_loss_cls, tgt_DA_ins_loss_cls, \
             DA_cst_loss, tgt_DA_cst_loss = da
         return (rois, cls_prob, bbox_pred, rpn_loss_cls, rpn_loss_bbox, RCNN_loss_cls,

@@ -64,9 +64,10 @@ def _grad_pair(*gs):
         return g0
     z = None
     out = []
+    dev = next(g.device for g in gs if g is not None)
     for g in gs:
         if g is None:
-            z = z if z is not None else torch.zeros((), dtype=torch.float32, device=gs[0].device)
+            z = z if z is not None else torch.zeros((), dtype=torch.float32, device=dev)
             g = z
         out.append(g.reshape(()).float())
     return torch.stack(out)
@@ -74,24 +75,28 @@ def _grad_pair(*gs):
 
 class RPNLossFunction(torch.autograd.Function):
     """(rpn_loss_cls, rpn_loss_box) of _RPN (rpn.py:89-108) from the raw RPN_cls_score
-    (B, 2A, H, W) and RPN_bbox_pred: tlod_rpn_loss_f32 / _bwd_f32."""
+    (B_total, 2A, H, W) and RPN_bbox_pred: tlod_rpn_loss_f32 / _bwd_f32.  The loss covers
+    the first B = labels.shape[0] images (the source image of a batched source + target
+    head pass); the gradients cover all B_total, so no slice enters the autograd graph."""
 
     @staticmethod
     def forward(ctx, score, bbox, labels, targets, inside, outside, sigma):
         from .. import _lib
         _lib.require_cuda(score, bbox, labels, targets, inside, outside)
-        B, twoA, H, W = score.shape
+        B_total, twoA, H, W = score.shape
         A = twoA // 2
+        B = labels.shape[0]
         t = [x.detach().contiguous().float() for x in (score, bbox, labels, targets, inside,
                                                        outside)]
-        assert t[1].shape == (B, 4 * A, H, W) and t[2].numel() == B * A * H * W
+        assert t[1].shape == (B_total, 4 * A, H, W) and t[2].numel() == B * A * H * W
+        assert B <= B_total and t[3].shape == (B, 4 * A, H, W)
         loss = torch.empty(3, dtype=torch.float32, device=score.device)  # cls, box, count
         L = _lib.lib()
         abi = [t[0], t[2], t[1], t[3], t[4], t[5]]  # score, labels, bbox, targets, in, out
         _lib.check(L.tlod_rpn_loss_f32(*[_lib.ptr(x) for x in abi], B, A, H, W, float(sigma),
                                        _lib.ptr(loss), _lib.ptr(loss[2:]), _lib.stream_of(score)),
                    "rpn_loss")
-        ctx.sigma, ctx.dims = sigma, (B, A, H, W)
+        ctx.sigma, ctx.dims = sigma, (B, B_total, A, H, W)
         ctx.save_for_backward(*t, loss)
         return loss[0], loss[1]
 
@@ -99,13 +104,13 @@ class RPNLossFunction(torch.autograd.Function):
     def backward(ctx, g_cls, g_box):
         from .. import _lib
         *t, loss = ctx.saved_tensors
-        B, A, H, W = ctx.dims
+        B, B_total, A, H, W = ctx.dims
         g = _grad_pair(g_cls, g_box)
         dscore = torch.empty_like(t[0])
         dbbox = torch.empty_like(t[1])
         L = _lib.lib()
         abi = [t[0], t[2], t[1], t[3], t[4], t[5]]
-        _lib.check(L.tlod_rpn_loss_bwd_f32(*[_lib.ptr(x) for x in abi], B, A, H, W,
+        _lib.check(L.tlod_rpn_loss_bwd_f32(*[_lib.ptr(x) for x in abi], B, B_total, A, H, W,
                                            float(ctx.sigma), _lib.ptr(g), _lib.ptr(loss[2:]),
                                            _lib.ptr(dscore), _lib.ptr(dbbox),
                                            _lib.stream_of(dscore)), "rpn_loss_bwd")
@@ -125,13 +130,15 @@ class RCNNLossFunction(torch.autograd.Function):
     def forward(ctx, cls_score, bbox_pred, labels, targets, inside, outside, agnostic, sigma):
         from .. import _lib
         _lib.require_cuda(cls_score, bbox_pred, labels, targets, inside, outside)
-        R, C = cls_score.shape
+        ctx.set_materialize_grads(False)  # cls_prob / gathered boxes get no gradient
+        R_total, C = cls_score.shape
+        R = labels.numel()  # the loss covers the first R rows (the source RoIs)
         cs, bp = cls_score.detach().contiguous().float(), bbox_pred.detach().contiguous().float()
         lab = labels.detach().contiguous().long()
         tg, iw, ow = (x.detach().contiguous().float() for x in (targets, inside, outside))
-        assert bp.shape == (R, 4 if agnostic else 4 * C) and lab.numel() == R
+        assert bp.shape == (R_total, 4 if agnostic else 4 * C) and R <= R_total
         assert tg.shape == iw.shape == ow.shape == (R, 4)
-        prob = torch.empty_like(cs)
+        prob = torch.empty((R, C), dtype=torch.float32, device=cs.device)
         sel = torch.empty((R, 4), dtype=torch.float32, device=cs.device)
         loss = torch.empty(2, dtype=torch.float32, device=cs.device)
         L = _lib.lib()
@@ -139,7 +146,7 @@ class RCNNLossFunction(torch.autograd.Function):
                                         _lib.ptr(iw), _lib.ptr(ow), R, C, int(agnostic),
                                         float(sigma), _lib.ptr(prob), _lib.ptr(sel),
                                         _lib.ptr(loss), _lib.stream_of(cs)), "rcnn_loss")
-        ctx.agnostic, ctx.sigma = agnostic, sigma
+        ctx.agnostic, ctx.sigma, ctx.R_total = agnostic, sigma, R_total
         ctx.save_for_backward(prob, bp, lab, tg, iw, ow)
         ctx.mark_non_differentiable(prob, sel)
         return prob, sel, loss[0], loss[1]
@@ -149,11 +156,15 @@ class RCNNLossFunction(torch.autograd.Function):
         from .. import _lib
         prob, bp, lab, tg, iw, ow = ctx.saved_tensors
         R, C = prob.shape
+        if g_cls is None and g_box is None:
+            return None, None, None, None, None, None, None, None
         g = _grad_pair(g_cls, g_box)
-        dcls, dbox = torch.empty_like(prob), torch.empty_like(bp)
+        dcls = torch.empty((ctx.R_total, C), dtype=torch.float32, device=prob.device)
+        dbox = torch.empty_like(bp)
         L = _lib.lib()
         _lib.check(L.tlod_rcnn_loss_bwd_f32(_lib.ptr(prob), _lib.ptr(bp), _lib.ptr(lab),
-                                            _lib.ptr(tg), _lib.ptr(iw), _lib.ptr(ow), R, C,
+                                            _lib.ptr(tg), _lib.ptr(iw), _lib.ptr(ow), R,
+                                            ctx.R_total, C,
                                             int(ctx.agnostic), float(ctx.sigma), _lib.ptr(g),
                                             _lib.ptr(dcls), _lib.ptr(dbox),
                                             _lib.stream_of(prob)), "rcnn_loss_bwd")
@@ -162,8 +173,9 @@ class RCNNLossFunction(torch.autograd.Function):
 
 def rcnn_losses(cls_score, bbox_pred, labels, targets, inside, outside, agnostic=False,
                 sigma=1.0):
-    """Training-mode head losses: returns (cls_prob, bbox_pred gathered at the label's
-    class (a copy of bbox_pred when class-agnostic), loss_cls, loss_bbox).  cls_prob and
+    """Training-mode head losses over the first labels.numel() rows of cls_score /
+    bbox_pred: returns (cls_prob, bbox_pred gathered at the label's class (a copy of
+    bbox_pred when class-agnostic), loss_cls, loss_bbox) for those rows.  cls_prob and
     the gathered boxes are outputs only (no gradient flows back through them, as in
     training, where only the losses are differentiated)."""
     return RCNNLossFunction.apply(cls_score, bbox_pred, labels, targets, inside, outside,
@@ -215,6 +227,59 @@ class DALossFunction(torch.autograd.Function):
                                           _lib.ptr(dt), _lib.ptr(di_s), _lib.ptr(di_t),
                                           _lib.stream_of(ss)), "da_loss_bwd")
         return (ds, dt, di_s.view(ctx.ins_shapes[0]), di_t.view(ctx.ins_shapes[1]), None, None)
+
+
+class DALossPackedFunction(torch.autograd.Function):
+    """DALossFunction with the two domains packed along the batch / row axis of one image
+    score tensor (Bs + Bt, 2, H, W) and one instance tensor (n_s + n_t, 1) — the layout of
+    DAF's batched source + target pass — so each gets one gradient tensor and no slice
+    enters the autograd graph."""
+
+    @staticmethod
+    def forward(ctx, score2, ins2, Bs, n_s, need_s, need_t):
+        from .. import _lib
+        _lib.require_cuda(score2, ins2)
+        sc = score2.detach().contiguous().float()
+        ins = ins2.detach().contiguous().float().view(-1)
+        B2, c2, H, W = sc.shape
+        Bt, n_t = B2 - Bs, ins.numel() - n_s
+        need = [x.detach().to(sc.device).contiguous().float().view(-1) for x in (need_s, need_t)]
+        assert c2 == 2 and Bt > 0 and n_t >= 0 and need[0].numel() == Bs and need[1].numel() == Bt
+        out = torch.empty(8, dtype=torch.float32, device=sc.device)
+        img = 2 * H * W * 4  # bytes per image of score2
+        L = _lib.lib()
+        _lib.check(L.tlod_da_loss_f32(_lib.ptr(sc), _lib.c_void_p(sc.data_ptr() + Bs * img),
+                                      _lib.ptr(need[0]), _lib.ptr(need[1]), _lib.ptr(ins),
+                                      _lib.c_void_p(ins.data_ptr() + 4 * n_s), Bs, Bt, H, W, H,
+                                      W, n_s, n_t, _lib.ptr(out), _lib.ptr(out[6:]),
+                                      _lib.stream_of(sc)), "da_loss")
+        ctx.dims = (Bs, Bt, H, W, n_s, n_t)
+        ctx.ins_shape = ins2.shape
+        ctx.save_for_backward(sc, ins, need[0], need[1], out)
+        return out[0], out[1], out[3], out[4], out[2], out[5]
+
+    @staticmethod
+    def backward(ctx, g_img_s, g_ins_s, g_img_t, g_ins_t, g_cst_s, g_cst_t):
+        from .. import _lib
+        sc, ins, need_s, need_t, out = ctx.saved_tensors
+        Bs, Bt, H, W, n_s, n_t = ctx.dims
+        g = torch.stack([x.reshape(()) if x is not None else out.new_zeros(())
+                         for x in (g_img_s, g_ins_s, g_cst_s, g_img_t, g_ins_t, g_cst_t)])
+        dsc, dins = torch.empty_like(sc), torch.empty_like(ins)
+        img = 2 * H * W * 4
+        L = _lib.lib()
+        _lib.check(L.tlod_da_loss_bwd_f32(
+            _lib.ptr(sc), _lib.c_void_p(sc.data_ptr() + Bs * img), _lib.ptr(need_s),
+            _lib.ptr(need_t), _lib.ptr(ins), _lib.c_void_p(ins.data_ptr() + 4 * n_s), Bs, Bt, H,
+            W, H, W, n_s, n_t, _lib.ptr(g), _lib.ptr(out[6:]), _lib.ptr(dsc),
+            _lib.c_void_p(dsc.data_ptr() + Bs * img), _lib.ptr(dins),
+            _lib.c_void_p(dins.data_ptr() + 4 * n_s), _lib.stream_of(sc)), "da_loss_bwd")
+        return dsc, dins.view(ctx.ins_shape), None, None, None, None
+
+
+def daf_da_losses_packed(score2, ins2, Bs, n_s, need_s, need_t):
+    """daf_da_losses for the packed (source rows first) layout of DALossPackedFunction."""
+    return DALossPackedFunction.apply(score2, ins2, int(Bs), int(n_s), need_s, need_t)
 
 
 def daf_da_losses(base_score_s, base_score_t, ins_s, ins_t, need_s, need_t):

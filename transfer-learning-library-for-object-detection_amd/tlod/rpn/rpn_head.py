@@ -48,14 +48,19 @@ class _RPN(nn.Module):
         bbox = self.RPN_bbox_pred(rpn_conv1)
         return rpn_cls_score, score_reshape, prob, bbox
 
-    def losses(self, rpn_cls_score, score_reshape, bbox, gt_boxes, im_info, num_boxes, rng=None):
-        B = rpn_cls_score.size(0)
+    def losses(self, rpn_cls_score, score_reshape, bbox, gt_boxes, im_info, num_boxes, rng=None,
+               n_images=None):
+        """RPN losses of the first ``n_images`` images of a (possibly larger) head batch
+        (default: all); the fused path differentiates the whole batch tensors (zero
+        gradient for the other images) so no slice enters the autograd graph."""
+        B = rpn_cls_score.size(0) if n_images is None else int(n_images)
         labels, targets, inside, outside = self.RPN_anchor_target(
-            (rpn_cls_score.detach(), gt_boxes, im_info, num_boxes), rng=rng)
+            (rpn_cls_score[:B].detach(), gt_boxes, im_info, num_boxes), rng=rng)
         if fused_losses():
             loss_cls, loss_box = rpn_losses(rpn_cls_score, bbox, labels, targets, inside,
                                             outside, sigma=3.0)
             return loss_cls, loss_box, labels
+        score_reshape, bbox = score_reshape[:B], bbox[:B]
         scores = score_reshape.permute(0, 2, 3, 1).contiguous().view(-1, 2)
         loss_cls = masked_cross_entropy(scores, labels.view(B, -1).view(-1))
         loss_box = smooth_l1_loss(bbox, targets, inside, outside, sigma=3, dim=[1, 2, 3])
