@@ -357,6 +357,16 @@ int tlod_space_to_depth_f32(const float* x, int B, int C, int H, int W, int scal
 int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int W, int scale, float* dx,
                             tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ FC head activation
+ * Replaces: nn.ReLU(inplace) + nn.Dropout(p) after the head's Linear layers
+ *   (lib/DAF/vgg16.py:67-71, lib/DAF/DA.py:53-73).  out = y > 0 and kept ? y / (1 - p) : 0,
+ *   kept <=> a counter-based uniform(seed, i) >= p (p = 0: plain ReLU).  Backward:
+ *   g = out > 0 ? dout / (1 - p) : 0 (the mask is recovered from out, never stored). */
+int tlod_relu_dropout_f32(const float* y, float* out, long long n, float p,
+                          unsigned long long seed, tlod_stream_t stream);
+int tlod_relu_dropout_bwd_f32(const float* dout, const float* out, float* g, long long n,
+                              float p, tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ Fused losses
  * One forward launch (single workgroup, fixed-order double accumulation: deterministic)
  * and one backward launch (writes every gradient element) per loss family.  grad_loss

@@ -85,3 +85,28 @@ def test_linear_state_dict_matches_nn_linear():
     a, b = Linear(25088, 4096), torch.nn.Linear(25088, 4096)
     assert a.state_dict().keys() == b.state_dict().keys()
     assert a.weight.shape == b.weight.shape and a.bias.shape == b.bias.shape
+
+
+def test_relu_dropout_fused():
+    """tlod_relu_dropout_f32: p = 0 is exactly ReLU; at p = 0.5 about half the positive
+    entries survive, scaled by 2; the backward routes dout through exactly the surviving
+    entries (x2) — the same function torch's relu + dropout computes for that mask."""
+    from tlod.linear import ReluDropoutFunction
+    g = torch.Generator().manual_seed(0)
+    y = torch.randn(556, 4096, generator=g).to(dev)
+    out0 = ReluDropoutFunction.apply(y, 0.0, 123)
+    assert torch.equal(out0, torch.relu(y))
+    yr = y.clone().requires_grad_(True)
+    out = ReluDropoutFunction.apply(yr, 0.5, 123)
+    pos = y > 0
+    kept = out > 0
+    assert not bool((kept & ~pos).any())
+    frac = float(kept.sum()) / float(pos.sum())
+    assert abs(frac - 0.5) < 0.01, frac
+    assert torch.equal(out[kept], y[kept] * 2.0)
+    dout = torch.randn(y.shape, generator=g).to(dev)
+    out.backward(dout)
+    assert torch.equal(yr.grad, torch.where(kept, dout * 2.0, torch.zeros_like(dout)))
+    # same seed, same mask; another seed, another mask
+    assert torch.equal(ReluDropoutFunction.apply(y, 0.5, 123), out.detach())
+    assert not torch.equal(ReluDropoutFunction.apply(y, 0.5, 124), out.detach())

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from ..config import cfg
 from ..conv import Conv2d
-from ..linear import Linear
+from ..linear import Linear, relu_dropout
 from ..detector.losses import (daf_da_losses, daf_da_losses_packed, fused_losses, rcnn_losses,
                                smooth_l1_loss, weighted_loss_sum)
 from ..detector.vgg16 import vgg16_base, vgg16_top
@@ -102,8 +102,8 @@ class _InstanceDA(nn.Module):
     def score(self, x):
         """The sigmoid outputs alone (the DAF forward discards the label tensor)."""
         x = grad_reverse(x)
-        x = self.dc_drop1(self.dc_relu1(self.dc_ip1(x)))
-        x = self.dc_drop2(self.dc_relu2(self.dc_ip2(x)))
+        x = relu_dropout(self.dc_ip1(x), self.dc_drop1)
+        x = relu_dropout(self.dc_ip2(x), self.dc_drop2)
         return torch.sigmoid(self.clssifer(x))
 
     def forward(self, x, need_backprop):

@@ -10,7 +10,7 @@ GEMMs in libtlod).
 import torch.nn as nn
 
 from ..conv import Conv2d, vgg_init_
-from ..linear import Linear
+from ..linear import FcTop, Linear
 
 # split points (shared frozen prefix end, conv3 end, conv4 end) of RCNN_base for the MAF /
 # ATF taps: conv3 = features[:16], conv34 = [16:23], conv45 = [23:-1] (lib/MAF/vgg16.py:84-86)
@@ -53,4 +53,4 @@ def vgg16_top():
     for m in (fc6, fc7):  # torchvision VGG Linear init
         m.weight.data.normal_(0, 0.01)
         m.bias.data.zero_()
-    return nn.Sequential(fc6, nn.ReLU(True), nn.Dropout(), fc7, nn.ReLU(True), nn.Dropout())
+    return FcTop(fc6, nn.ReLU(True), nn.Dropout(), fc7, nn.ReLU(True), nn.Dropout())

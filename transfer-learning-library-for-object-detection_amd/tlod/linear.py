@@ -83,3 +83,62 @@ class Linear(nn.Linear):
         if m == "f32" or x.dim() != 2:
             return super().forward(x)
         return LinearFunction.apply(x, self.weight, self.bias, m)
+
+
+def fused_act():
+    """TLOD_FUSED_ACT (default 1): ReLU + dropout after the head's Linear layers as one
+    libtlod pass each way (tlod_relu_dropout_f32); 0 = nn.ReLU + nn.Dropout."""
+    return os.environ.get("TLOD_FUSED_ACT", "1") != "0"
+
+
+class ReluDropoutFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, p, seed):
+        _lib.require_cuda(y)
+        y = y.contiguous()
+        out = torch.empty_like(y)
+        _lib.check(_lib.lib().tlod_relu_dropout_f32(_lib.ptr(y), _lib.ptr(out), y.numel(), float(p),
+                                                    seed, _lib.stream_of(y)), "relu_dropout")
+        ctx.p = float(p)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (out,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        g = torch.empty_like(out)
+        _lib.check(_lib.lib().tlod_relu_dropout_bwd_f32(_lib.ptr(dout), _lib.ptr(out), _lib.ptr(g),
+                                                        out.numel(), ctx.p, _lib.stream_of(out)),
+                   "relu_dropout_bwd")
+        return g, None, None
+
+
+def relu_dropout(y, dropout):
+    """dropout(relu(y)) with the nn.Dropout module's p and training mode (its RNG stream is
+    libtlod's counter-based one, seeded from torch's CPU generator: no device sync)."""
+    p = float(dropout.p) if dropout.training else 0.0
+    if not fused_act():
+        return dropout(torch.relu(y))
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    return ReluDropoutFunction.apply(y, p, seed)
+
+
+class FcTop(nn.Sequential):
+    """nn.Sequential(Linear, ReLU, Dropout, Linear, ReLU, Dropout) — the VGG16 RCNN_top,
+    same modules and state_dict keys — whose Linear -> ReLU -> Dropout triples run as the
+    split-bf16 GEMM (bias in its epilogue) plus one fused ReLU + dropout pass."""
+
+    def forward(self, x):
+        mods = list(self)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if (i + 2 < len(mods) and isinstance(m, nn.Linear) and isinstance(mods[i + 1], nn.ReLU)
+                    and isinstance(mods[i + 2], nn.Dropout)):
+                x = relu_dropout(m(x), mods[i + 2])
+                i += 3
+            else:
+                x = m(x)
+                i += 1
+        return x
