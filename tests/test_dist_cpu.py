@@ -41,8 +41,10 @@ def _worker(rank, world, port, out):
     from tlod.dist import GradBucketReducer, init_from_env
     init_from_env(backend="gloo")
     m = _model(seed=rank)  # different init per rank: the reducer must broadcast rank 0's
-    red = GradBucketReducer(m, bucket_mb=0.004)  # ~1000 floats -> several buckets
-    assert len(red.buckets) >= 3
+    # ~130-float buckets for the small tensors; the two larger weights (2048 and 3072
+    # floats) are all-reduced directly on their autograd gradient tensors
+    red = GradBucketReducer(m, bucket_mb=0.0005, direct_numel=2000)
+    assert len(red.buckets) >= 2 and len(red.direct) == 2
     for step in range(2):
         red.zero_grad()
         x, y = _data(rank * 10 + step)

@@ -5,12 +5,16 @@ Replaces the reference's single-process ``nn.DataParallel`` (methods/DAF/DAF_tra
 GPU 0 through the host thread.  Here:
 
   * parameters are broadcast from rank 0 once at start;
-  * every trainable parameter's ``.grad`` is a view into a flat, bucket-contiguous
-    buffer, so autograd accumulates straight into the buffers RCCL reduces;
-  * a post-accumulate-grad hook counts ready parameters per bucket and launches an async
-    all-reduce (ReduceOp.AVG on RCCL — the DataParallel loss.mean() semantics) as soon
-    as a bucket is complete, overlapping communication with the rest of the backward
-    (the large fc6/fc7 buckets complete first: the heads backprop before the backbone);
+  * large parameters (>= ``direct_numel`` elements: the conv and fc weights, 98% of the
+    568 MB) are all-reduced in place as single messages from their post-accumulate-grad
+    hook, on the gradient tensor autograd produced (set_to_none: no zero fill, no
+    accumulate-add, no copy into a bucket);
+  * the small ones (biases, the narrow heads) have ``.grad`` views into flat buckets so
+    they travel in few messages; a hook counts ready parameters per bucket and launches
+    the bucket's async all-reduce when it is complete;
+  * every all-reduce is async (ReduceOp.AVG on RCCL — the DataParallel loss.mean()
+    semantics) and overlaps the rest of the backward (fc6/fc7 are ready first: the heads
+    backprop before the backbone);
   * ``finish()`` waits for the outstanding buckets before clip_gradient / SGD, which
     then run on identical gradients on every rank (no extra collective for the norm).
 
@@ -41,10 +45,12 @@ def init_from_env(backend=None):
 
 
 class GradBucketReducer:
-    def __init__(self, model, bucket_mb=64.0, group=None):
+    def __init__(self, model, bucket_mb=64.0, group=None, direct_numel=1 << 20):
         self.group = group
         self.world = dist.get_world_size(group)
         self.params = [p for p in model.parameters() if p.requires_grad]
+        self.direct = {p for p in self.params if p.numel() >= direct_numel}
+        self.direct_work = []
         backend = dist.get_backend(group)
         self.avg = backend == "nccl"
         # broadcast initial weights (and buffers) from rank 0
@@ -54,7 +60,7 @@ class GradBucketReducer:
         # buckets in reverse registration order (~ gradient readiness order)
         cap = int(bucket_mb * 1024 * 1024 / 4)
         buckets, cur, cur_n = [], [], 0
-        for p in reversed(self.params):
+        for p in reversed([q for q in self.params if q not in self.direct]):
             if cur and cur_n + p.numel() > cap:
                 buckets.append(cur)
                 cur, cur_n = [], 0
@@ -80,12 +86,20 @@ class GradBucketReducer:
             b["flat"].zero_()
             b["ready"] = 0
             b["work"] = None
+        for p in self.direct:
+            p.grad = None
+        self.direct_work = []
 
     def _launch(self, b):
         op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
         b["work"] = dist.all_reduce(b["flat"], op=op, group=self.group, async_op=True)
 
     def _on_grad(self, p):
+        if p in self.direct:
+            op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+            self.direct_work.append(
+                (p, dist.all_reduce(p.grad, op=op, group=self.group, async_op=True)))
+            return
         b = self.buckets[self.bucket_of[p]]
         b["ready"] += 1
         if b["ready"] == len(b["params"]):
@@ -101,6 +115,14 @@ class GradBucketReducer:
                 b["flat"].div_(self.world)
             b["work"] = None
             b["ready"] = 0
-        # grads must still alias the flat buffers (optimizer.zero_grad(set_to_none=False))
+        for p, w in self.direct_work:
+            w.wait()
+            if not self.avg:
+                p.grad.div_(self.world)
+        if len(self.direct_work) != len(self.direct):
+            raise RuntimeError("GradBucketReducer: a large parameter received no gradient this "
+                               "step (every rank must all-reduce the same tensors)")
+        self.direct_work = []
+        # small grads must still alias the flat buffers (zero them with reducer.zero_grad())
         for p in self.params:
             assert p.grad is not None
