@@ -74,18 +74,39 @@ rpn_loss_fwd_kernel(const float* __restrict__ score, const float* __restrict__ l
   __shared__ double sh[16 * 3];
   double v[3] = {0.0, 0.0, 0.0};  // ce sum, kept rows, smooth-l1 sum
   const long long rows = (long long)B * AHW;
-  for (long long r = threadIdx.x; r < rows; r += blockDim.x) {
-    const float lab = labels[r];
-    if (lab == -1.f) continue;
-    const long long b = r / AHW, q = r - b * AHW;
-    const float s0 = score[b * 2 * AHW + q], s1 = score[b * 2 * AHW + AHW + q];
-    const LogSoftmax2 ls(s0, s1);
-    v[0] -= (double)((long long)lab == 1 ? ls.l1 : ls.l0);
-    v[1] += 1.0;
+  // one workgroup (fixed-order reduction); 4 rows in flight per thread so the label loads
+  // of a mostly-ignored (-1) anchor set do not serialise on memory latency
+  for (long long r0 = threadIdx.x; r0 < rows; r0 += 4LL * blockDim.x) {
+    float lab[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long r = r0 + (long long)u * blockDim.x;
+      lab[u] = r < rows ? labels[r] : -1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (lab[u] == -1.f) continue;
+      const long long r = r0 + (long long)u * blockDim.x;
+      const long long b = r / AHW, q = r - b * AHW;
+      const float s0 = score[b * 2 * AHW + q], s1 = score[b * 2 * AHW + AHW + q];
+      const LogSoftmax2 ls(s0, s1);
+      v[0] -= (double)((long long)lab[u] == 1 ? ls.l1 : ls.l0);
+      v[1] += 1.0;
+    }
   }
-  const long long ne = rows * 4;
-  for (long long i = threadIdx.x; i < ne; i += blockDim.x)
-    v[2] += (double)smooth_l1(bbox[i], tgt[i], inw[i], outw[i], s2, nullptr);
+  // box terms: rows x 4 contiguous floats per operand, read as float4 (torch allocations
+  // are 16-B aligned)
+  const float4* b4 = reinterpret_cast<const float4*>(bbox);
+  const float4* t4 = reinterpret_cast<const float4*>(tgt);
+  const float4* i4 = reinterpret_cast<const float4*>(inw);
+  const float4* o4 = reinterpret_cast<const float4*>(outw);
+  for (long long i = threadIdx.x; i < rows; i += blockDim.x) {
+    const float4 p = b4[i], t = t4[i], iw = i4[i], ow = o4[i];
+    v[2] += (double)smooth_l1(p.x, t.x, iw.x, ow.x, s2, nullptr);
+    v[2] += (double)smooth_l1(p.y, t.y, iw.y, ow.y, s2, nullptr);
+    v[2] += (double)smooth_l1(p.z, t.z, iw.z, ow.z, s2, nullptr);
+    v[2] += (double)smooth_l1(p.w, t.w, iw.w, ow.w, s2, nullptr);
+  }
   block_sum<3>(v, sh);
   if (threadIdx.x == 0) {
     const double kept = v[1] > 1.0 ? v[1] : 1.0;
@@ -313,6 +334,9 @@ int tlod_rpn_loss_f32(const float* score, const float* labels, const float* bbox
   TLOD_CHECK_ARG(score && labels && bbox && targets && inside && outside && loss && count,
                  "null pointer");
   TLOD_CHECK_ARG(B > 0 && A > 0 && H > 0 && W > 0 && sigma > 0.f, "bad shape / sigma");
+  TLOD_CHECK_ARG(((uintptr_t)bbox | (uintptr_t)targets | (uintptr_t)inside | (uintptr_t)outside) %
+                         16 == 0,
+                 "box operands must be 16-byte aligned");
   rpn_loss_fwd_kernel<<<1, kRedThreads, 0, (hipStream_t)stream>>>(
       score, labels, bbox, targets, inside, outside, B, A * H * W, sigma * sigma, loss, count);
   TLOD_LAUNCH_CHECK();

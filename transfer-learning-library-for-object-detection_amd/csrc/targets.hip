@@ -218,24 +218,33 @@ __global__ void __launch_bounds__(256) at_iou_kernel(AnchorGeo geo, const float*
   for (int g = threadIdx.x; g < G; g += blockDim.x) bmax[g] = f2ord(-INFINITY);
   __syncthreads();
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  bool ins = false;
   if (idx < N) {
-    float a[4];
     geo.box(idx, a);
-    if (anchor_inside(a, im_info[1], im_info[0], border)) {
-      const float ax = a[2] - a[0] + 1.f, ay = a[3] - a[1] + 1.f;
-      const float area = ax * ay;
-      const bool az = (ax == 1.f) && (ay == 1.f);
-      float best = 0.f;
-      int barg = 0;
-      for (int g = 0; g < G; ++g) {
-        const float o = overlap(a[0], a[1], a[2], a[3], area, az, s.x1[g], s.y1[g], s.x2[g],
-                                s.y2[g], s.area[g], s.zero[g]);
-        if (g == 0 || o > best) { best = o; barg = g; }
-        atomicMax(&bmax[g], f2ord(o));
-      }
-      maxov[(size_t)b * N + idx] = best;
-      argmax[(size_t)b * N + idx] = barg;
-    }
+    ins = anchor_inside(a, im_info[1], im_info[0], border);
+  }
+  // wave-uniform loop: each gt's max over the wave's inside anchors is reduced across the
+  // 64 lanes first (max is order-free: same result as per-anchor atomics), then one LDS
+  // atomic per wave instead of 64 contending on the same address
+  const float ax = a[2] - a[0] + 1.f, ay = a[3] - a[1] + 1.f;
+  const float area = ax * ay;
+  const bool az = (ax == 1.f) && (ay == 1.f);
+  const uint32_t kNone = f2ord(-INFINITY);
+  float best = 0.f;
+  int barg = 0;
+  for (int g = 0; g < G; ++g) {
+    const float o = overlap(a[0], a[1], a[2], a[3], area, az, s.x1[g], s.y1[g], s.x2[g],
+                            s.y2[g], s.area[g], s.zero[g]);
+    if (g == 0 || o > best) { best = o; barg = g; }
+    uint32_t v = ins ? f2ord(o) : kNone;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    if ((threadIdx.x & 63) == 0 && v != kNone) atomicMax(&bmax[g], v);
+  }
+  if (ins) {
+    maxov[(size_t)b * N + idx] = best;
+    argmax[(size_t)b * N + idx] = barg;
   }
   __syncthreads();
   for (int g = threadIdx.x; g < G; g += blockDim.x)
@@ -262,6 +271,7 @@ __global__ void __launch_bounds__(256) at_label_kernel(AnchorGeo geo, const floa
   if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
   __syncthreads();
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  int lab = -2;  // past the end: counts nowhere
   if (idx < N) {
     float a[4];
     geo.box(idx, a);
@@ -279,10 +289,15 @@ __global__ void __launch_bounds__(256) at_label_kernel(AnchorGeo geo, const floa
       if (tie) l = 1;
       if (mo >= cfg.pos_overlap) l = 1;
       if (cfg.clobber_positives && mo < cfg.neg_overlap) l = 0;
-      if (l == 1) atomicAdd(&cnt[0], 1);
-      if (l == 0) atomicAdd(&cnt[1], 1);
     }
     label[(size_t)b * N + idx] = l;
+    lab = l;
+  }
+  // per-wave ballot counts: one LDS atomic per wave and class
+  const int n1 = __popcll(__ballot(lab == 1)), n0 = __popcll(__ballot(lab == 0));
+  if ((threadIdx.x & 63) == 0) {
+    if (n1) atomicAdd(&cnt[0], n1);
+    if (n0) atomicAdd(&cnt[1], n0);
   }
   __syncthreads();
   if (threadIdx.x < 2 && cnt[threadIdx.x]) atomicAdd(&counts[b * 2 + threadIdx.x], cnt[threadIdx.x]);
