@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1200)
     ap.add_argument("--cpu-baseline-steps", type=int, default=2,
                     help="oracle CPU steps timed on rank 0 at N=1 (0 disables)")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--net", choices=("vgg16", "res101"), default="vgg16")
     ap.add_argument("--method", choices=("daf", "maf", "atf"), default="daf",
                     help="detector (the headline metric is DAF; MAF / ATF are secondary workloads)")
@@ -145,8 +145,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     losses = []
+    sync = os.environ.get("TLOD_BENCH_SYNC") == "1"  # A/B: host waits for every step
     for _ in range(a.steps):
         losses.append(train_step(model, opt, data.next(), reducer=reducer))
+        if sync:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -329,7 +329,9 @@ int tlod_upsample2_zero_f32(const float* dy, int N, int C, int H, int W, float* 
  * Replaces: clip_gradient(model, 10.) lib/model/utils/net_utils.py:38-49 (per-param norm
  *   loop + .item() host sync) + torch.optim.SGD(momentum) methods/DAF/DAF_train.py:323,408.
  * chunks: device array of n_chunks descriptors (each <= 65536 elements of one tensor);
- * per element: g' = g * clip/max(||G||, clip); d = g' + wd*p; buf = m*buf + d; p -= lr*buf
+ * per element: g = grad_scale * grad (data parallel: 1/world of the all-reduced sum, the
+ * DataParallel loss.mean() semantics; 1 otherwise); g' = g * clip/max(||g||, clip);
+ * d = g' + wd*p; buf = m*buf + d; p -= lr*buf
  * (torch SGD semantics, dampening 0; buf starts at 0, so step 1 gives buf = d).
  * clip_norm <= 0 disables clipping.  partials: float[n_chunks] scratch.  norm_scale: 2
  * device floats receiving (total grad norm, applied scale).  Deterministic. */
@@ -342,8 +344,27 @@ typedef struct tlod_sgd_chunk {
   float weight_decay;
 } tlod_sgd_chunk;
 
-int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float momentum,
-                      float clip_norm, float* partials, float* norm_scale, tlod_stream_t stream);
+int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float grad_scale,
+                      float momentum, float clip_norm, float* partials, float* norm_scale,
+                      tlod_stream_t stream);
+
+/* ------------------------------------------------------------------ Input blob
+ * Replaces: the data layer's per-image host chain — scipy imread (RGB) -> BGR -> flip
+ *   (lib/roi_data_layer/minibatch.py:62-82) -> astype(float32) -= PIXEL_MEANS ->
+ *   cv2.resize(fx = fy = im_scale, INTER_LINEAR) (lib/model/utils/blob.py:35-52) -> crop /
+ *   zero-pad to the aspect group's shape, HWC -> CHW (lib/roi_data_layer/roibatchLoader.py:
+ *   94-207).  src: decoded RGB image, H x W x 3 uint8 on the device.  lut: 3 x 256 float,
+ *   lut[c*256 + v] = float32(v - PIXEL_MEANS[c]) for BGR channel c (rounded once from
+ *   double, as numpy's in-place float32 -= float64).  xtab (Wr entries) / ytab (Hr
+ *   entries): device arrays of {int i0, int i1, float w0, float w1} — the cv::resize
+ *   INTER_LINEAR source index pair and weights of each resized column / row, flip already
+ *   applied to the column indices; every index must lie in [0, W) / [0, H) (the host
+ *   builds them, tlod/data/blob.py).  The kept region is Hd x Wd at (y0, x0) of the Hr x Wr
+ *   resized image (y0 + Hd <= Hr, x0 + Wd <= Wr).  out: 3 x Ho x Wo float32,
+ *   out[c][y][x] = resized[y + y0][x + x0][c] for y < Hd, x < Wd, else 0 (zero padding). */
+int tlod_image_blob_u8(const uint8_t* src, int H, int W, const float* lut, const void* xtab,
+                       const void* ytab, int Hr, int Wr, int y0, int x0, int Hd, int Wd, int Ho,
+                       int Wo, float* out, tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ MAF DRM
  * Replaces: the chunk / reshape / cat loops of DRM.forward, lib/MAF/drm.py:23-40 (a
@@ -364,6 +385,8 @@ int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int W, int sca
  *   g = out > 0 ? dout / (1 - p) : 0 (the mask is recovered from out, never stored). */
 int tlod_relu_dropout_f32(const float* y, float* out, long long n, float p,
                           unsigned long long seed, tlod_stream_t stream);
+/* Backward precondition: dout, out and g are 16-byte aligned (float4 path); else the
+ * call returns an argument error.  NaN inputs pass through both ways (torch semantics). */
 int tlod_relu_dropout_bwd_f32(const float* dout, const float* out, float* g, long long n,
                               float p, tlod_stream_t stream);
 
@@ -381,6 +404,9 @@ int tlod_relu_dropout_bwd_f32(const float* dout, const float* out, float* g, lon
  *   Backward: score / bbox may hold B_total >= B images of which the first B are the
  *   loss's; dscore (B_total, 2A, H, W) and dbbox (B_total, 4A, H, W) are written in full
  *   (zero past image B). */
+/* Precondition (both RPN calls): bbox, targets, inside and outside are contiguous
+ * (B, 4A, H, W) tensors at 16-byte aligned addresses (the box terms are read as float4);
+ * a misaligned pointer returns an argument error. */
 int tlod_rpn_loss_f32(const float* score, const float* labels, const float* bbox,
                       const float* targets, const float* inside, const float* outside, int B,
                       int A, int H, int W, float sigma, float* loss, float* count,

@@ -23,16 +23,23 @@ CFG = dict(pre_train=12000, post_train=2000, pre_test=6000, post_test=300, nms=0
 
 
 class _RoIAlignAvgCPU(torch.autograd.Function):
+    """float32 features: the CUDA kernels' arithmetic; float64 features (the exact-arithmetic
+    reference of the gradient bars): the same sample geometry in double."""
+
     @staticmethod
     def forward(ctx, feat, rois):
         f = feat.detach().numpy()
-        r = rois.detach().numpy()
-        ctx.meta = (r, f.shape)
+        r = rois.detach().float().numpy()
+        ctx.meta = (r, f.shape, f.dtype)
+        if f.dtype == np.float64:
+            return torch.from_numpy(oroi.roi_align_avg_fwd64(f, r, CFG["pool"], CFG["pool"], 1 / 16))
         return torch.from_numpy(oroi.roi_align_avg_fwd(f, r, CFG["pool"], CFG["pool"], 1 / 16))
 
     @staticmethod
     def backward(ctx, g):
-        r, (B, C, H, W) = ctx.meta
+        r, (B, C, H, W), dt = ctx.meta
+        if dt == np.float64:
+            return torch.from_numpy(oroi.roi_align_avg_bwd64(g.numpy(), r, B, C, H, W, 1 / 16)), None
         return torch.from_numpy(oroi.roi_align_avg_bwd(g.numpy(), r, B, C, H, W, 1 / 16)), None
 
 
@@ -154,7 +161,8 @@ class OracleDAF(nn.Module):
         c = CFG
         c3, c4, base = self._backbone(im)
         score, sr, prob, bbox = self._rpn(base)
-        rois = orpn.proposal_layer(prob.detach().numpy(), bbox.detach().numpy(), info.numpy(),
+        gt, info = gt.float(), info.float()  # the sampling ops see the reference's float32
+        rois = orpn.proposal_layer(prob.detach().float().numpy(), bbox.detach().float().numpy(), info.numpy(),
                                    self.base_anchors, c["stride"], c["pre_train"], c["post_train"],
                                    c["nms"])
         if rois_override is not None:
@@ -181,8 +189,8 @@ class OracleDAF(nn.Module):
         # target image: RPN in eval mode (TEST proposals)
         t_c3, t_c4, t_base = self._backbone(t_im)
         _, _, t_prob, t_bbox = self._rpn(t_base)
-        t_rois = orpn.proposal_layer(t_prob.detach().numpy(), t_bbox.detach().numpy(),
-                                     t_info.numpy(), self.base_anchors, c["stride"], c["pre_test"],
+        t_rois = orpn.proposal_layer(t_prob.detach().float().numpy(), t_bbox.detach().float().numpy(),
+                                     t_info.float().numpy(), self.base_anchors, c["stride"], c["pre_test"],
                                      c["post_test"], c["nms"])
         if rois_override is not None:
             t_rois = rois_override[1]

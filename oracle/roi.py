@@ -230,3 +230,50 @@ def roi_pool_bwd(top_grad, argmax, rois, B, C, H, W, scale):
         ok &= (ph >= phs) & (ph < phe) & (pw >= pws) & (pw < pwe)
         np.add.at(acc, idx[ok], g[ok])
     return acc.astype(np.float32).reshape(B, C, H, W)
+
+
+# ------------------------------------------------------------------ float64 reference
+# The same function in float64 arithmetic: the sample geometry (bin positions, integer
+# taps, fractional weights) is the kernels' float32 geometry — it defines which function
+# is computed — and every value / gradient operation after it is double.  Used as the
+# "exact" side of the gradient accuracy bars (tests/helpers.grad_error_bar).
+def roi_align_avg_fwd64(feat, rois, pooled_h, pooled_w, scale):
+    feat = np.asarray(feat, dtype=f64)
+    B, C, H, W = feat.shape
+    ah, aw = pooled_h + 1, pooled_w + 1
+    bidx, hs, ws, hr, wr, hv, wv = _align_geometry(rois, ah, aw, scale, H, W)
+    out = np.zeros((rois.shape[0], C, ah, aw), f64)
+    for r in range(rois.shape[0]):
+        f = feat[bidx[r]]
+        y = np.clip(hs[r], 0, H - 2)[:, None]
+        x = np.clip(ws[r], 0, W - 2)[None, :]
+        h_r, w_r = hr[r][:, None].astype(f64), wr[r][None, :].astype(f64)
+        v = (f[:, y, x] * (1 - h_r) * (1 - w_r) + f[:, y, x + 1] * (1 - h_r) * w_r
+             + f[:, y + 1, x] * h_r * (1 - w_r) + f[:, y + 1, x + 1] * h_r * w_r)
+        out[r] = np.where((hv[r][:, None] & wv[r][None, :])[None], v, 0.0)
+    return (out[..., :-1, :-1] + out[..., :-1, 1:] + out[..., 1:, :-1] + out[..., 1:, 1:]) / 4.0
+
+
+def roi_align_avg_bwd64(top_grad, rois, B, C, H, W, scale):
+    g = np.asarray(top_grad, dtype=f64) / 4.0
+    R, _, ph, pw = g.shape
+    ah, aw = ph + 1, pw + 1
+    ga = np.zeros((R, C, ah, aw), f64)
+    ga[..., :-1, :-1] += g
+    ga[..., :-1, 1:] += g
+    ga[..., 1:, :-1] += g
+    ga[..., 1:, 1:] += g
+    bidx, hs, ws, hr, wr, hv, wv = _align_geometry(rois, ah, aw, scale, H, W)
+    acc = np.zeros((B, C, H, W), f64)
+    for r in range(R):
+        valid = (hv[r][:, None] & wv[r][None, :])[None]
+        t = np.where(valid, ga[r], 0.0)
+        y = np.clip(hs[r], 0, H - 2)
+        x = np.clip(ws[r], 0, W - 2)
+        h_r, w_r = hr[r][:, None].astype(f64), wr[r][None, :].astype(f64)
+        for (dy, dx, wgt) in ((0, 0, (1 - h_r) * (1 - w_r)), (0, 1, (1 - h_r) * w_r),
+                              (1, 0, h_r * (1 - w_r)), (1, 1, h_r * w_r)):
+            yy = np.broadcast_to((y + dy)[:, None], (ah, aw)).reshape(-1)
+            xx = np.broadcast_to((x + dx)[None, :], (ah, aw)).reshape(-1)
+            np.add.at(acc[bidx[r]], (slice(None), yy, xx), (t * wgt).reshape(C, -1))
+    return acc

@@ -52,3 +52,33 @@ def rpn_outputs(rng, B, A, H, W, delta_scale=0.2):
     prob = p.reshape(B, 2 * A, H, W)
     deltas = (rng.normal(0, delta_scale, (B, 4 * A, H, W))).astype(np.float32)
     return prob, deltas
+
+
+def grad_errors(dev_named_params, o32, o64):
+    """Normwise relative error of each trainable gradient against the fp64 oracle run, for
+    the device (split-bf16 / fp32 kernels) and for the fp32 CPU oracle itself:
+    {name: (err_device, err_fp32_oracle)}."""
+    import torch
+    gp = dict(dev_named_params)
+    g64 = dict(o64.named_parameters())
+    out = {}
+    for k, p in o32.named_parameters():
+        if not p.requires_grad or p.grad is None:
+            continue
+        ref = g64[k].grad.double()
+        den = max(float(ref.norm()), 1e-30)
+        ed = float((gp[k].grad.detach().double().cpu() - ref).norm()) / den
+        e32 = float((p.grad.double() - ref).norm()) / den
+        out[k] = (ed, e32)
+    assert out, "no gradients compared"
+    _ = torch
+    return out
+
+
+def assert_grad_bar(errs, factor=2.0, floor=2e-6):
+    """the device gradient's error against fp64 is at most ``factor`` x
+    the fp32 CPU oracle's own error against fp64 (with an fp32-roundoff floor, for
+    gradients the fp32 oracle happens to reproduce almost exactly)."""
+    bad = {k: v for k, v in errs.items() if v[0] > factor * max(v[1], floor)}
+    assert not bad, {"violations": bad,
+                     "worst_ratio": max(v[0] / max(v[1], floor) for v in errs.values())}

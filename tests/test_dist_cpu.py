@@ -1,11 +1,12 @@
-"""tlod.dist.GradBucketReducer on CPU with the gloo backend, world_size 2: gradients
-after finish() equal the average of the per-rank gradients (the DataParallel loss.mean()
+"""tlod.dist.GradBucketReducer on CPU with the gloo backend, world_size 2: gradients after
+finish() equal the average of the per-rank gradients (the DataParallel loss.mean()
 semantics, methods/DAF/DAF_train.py:341-342 / :397), weights are broadcast from rank 0,
-and buckets launch from the post-accumulate hooks in any completion order."""
+and the buckets are launched in one static order even when the ranks' graphs finish their
+gradients in different orders (per-hook launches could pair different tensors
+across ranks)."""
 import os
 import socket
 
-import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -19,17 +20,36 @@ def _free_port():
     return p
 
 
+class Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.trunk = torch.nn.Linear(32, 64)
+        self.trunk.bias.requires_grad_(False)  # a frozen parameter must not break bucketing
+        self.head1 = torch.nn.Linear(64, 48)
+        self.head2 = torch.nn.Linear(64, 7)
+        self.unused = torch.nn.Linear(3, 3)  # never receives a gradient (ATF's RCNN_rpn_t)
+
+    def forward(self, x, swap):
+        h = torch.relu(self.trunk(x))
+        # the later-created branch is differentiated first: swapping the branch order swaps
+        # which head's gradients are ready first
+        if swap:
+            b = self.head2(h)
+            a = self.head1(h)
+        else:
+            a = self.head1(h)
+            b = self.head2(h)
+        return (a ** 2).mean() + (b ** 2).mean()
+
+
 def _model(seed):
     torch.manual_seed(seed)
-    m = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 48),
-                            torch.nn.ReLU(), torch.nn.Linear(48, 5))
-    m[0].bias.requires_grad_(False)  # a frozen parameter must not break bucketing
-    return m
+    return Net()
 
 
-def _data(rank):
-    g = torch.Generator().manual_seed(100 + rank)
-    return torch.randn(16, 32, generator=g), torch.randn(16, 5, generator=g)
+def _data(key):
+    g = torch.Generator().manual_seed(100 + key)
+    return torch.randn(16, 32, generator=g)
 
 
 def _worker(rank, world, port, out):
@@ -41,19 +61,22 @@ def _worker(rank, world, port, out):
     from tlod.dist import GradBucketReducer, init_from_env
     init_from_env(backend="gloo")
     m = _model(seed=rank)  # different init per rank: the reducer must broadcast rank 0's
-    # ~130-float buckets for the small tensors; the two larger weights (2048 and 3072
-    # floats) are all-reduced directly on their autograd gradient tensors
-    red = GradBucketReducer(m, bucket_mb=0.0005, direct_numel=2000)
-    assert len(red.buckets) >= 2 and len(red.direct) == 2
-    for step in range(2):
+    red = GradBucketReducer(m, bucket_mb=1e-5)  # ~10-float cap: one bucket per tensor
+    assert len(red.buckets) == len([p for p in m.parameters() if p.requires_grad])
+    orders = []
+    for step in range(3):
         red.zero_grad()
-        x, y = _data(rank * 10 + step)
-        loss = ((m(x) - y) ** 2).mean()
+        loss = m(_data(rank * 10 + step), swap=(rank == 1))
         loss.backward()
-        red.finish()
-        if step == 1:
-            out[rank] = {k: p.grad.clone() for k, p in m.named_parameters() if p.requires_grad}
-            out[f"w{rank}"] = {k: p.detach().clone() for k, p in m.named_parameters()}
+        orders.append(red.finish(scale=True))
+        out[f"g{rank}_{step}"] = {k: (None if p.grad is None else p.grad.clone())
+                                  for k, p in m.named_parameters() if p.requires_grad}
+        with torch.no_grad():
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.sub_(0.1 * p.grad)
+    out[f"order{rank}"] = orders
+    out[f"w{rank}"] = {k: p.detach().clone() for k, p in m.named_parameters()}
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,17 +86,28 @@ def test_reducer_gloo_world2():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
-    # reference: rank-0 weights, average of the two ranks' step-1 gradients
+    # the two ranks really did finish gradients in different orders
+    assert out["order0"][0] != out["order1"][0]
+    # reference: rank-0 weights, plain SGD on the average of the two ranks' gradients
     m = _model(seed=0)
-    grads = []
-    for rank in range(2):
-        m.zero_grad()
-        x, y = _data(rank * 10 + 1)
-        ((m(x) - y) ** 2).mean().backward()
-        grads.append({k: p.grad.clone() for k, p in m.named_parameters() if p.requires_grad})
-    for k in grads[0]:
-        ref = (grads[0][k] + grads[1][k]) / 2
-        torch.testing.assert_close(out[0][k], ref, rtol=1e-5, atol=1e-6)
-        torch.testing.assert_close(out[1][k], out[0][k], rtol=0, atol=0)
+    for step in range(3):
+        grads = []
+        for rank in range(2):
+            m.zero_grad(set_to_none=True)
+            m(_data(rank * 10 + step), swap=(rank == 1)).backward()
+            grads.append({k: p.grad.clone() for k, p in m.named_parameters()
+                          if p.requires_grad and p.grad is not None})
+        for rank in range(2):
+            got = out[f"g{rank}_{step}"]
+            assert got["unused.weight"] is None and got["unused.bias"] is None
+            for k in grads[0]:
+                ref = (grads[0][k] + grads[1][k]) * 0.5
+                torch.testing.assert_close(got[k], ref, rtol=1e-5, atol=1e-6)
+                assert torch.equal(got[k], out[f"g0_{step}"][k])
+        with torch.no_grad():
+            for k, p in m.named_parameters():
+                if k in grads[0]:
+                    p.sub_(0.1 * out[f"g0_{step}"][k])
     for k in out["w0"]:
         assert torch.equal(out["w0"][k], out["w1"][k])
+        assert torch.equal(out["w0"][k], dict(m.named_parameters())[k].detach())

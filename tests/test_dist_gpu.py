@@ -1,0 +1,105 @@
+"""Data-parallel DAF-VGG16 training on the real model: two processes on cuda:0 with gloo
+over device tensors (the one-GPU box stands in for two ranks; RCCL and gloo run the same
+reducer code — SUM all-reduce, 1/world applied by the fused optimizer).
+
+Checks after each of 2 steps of tlod.detector.train.train_step:
+  * weights are bit-identical on both ranks;
+  * they equal a single-process FusedSGDClip step on the two ranks' local gradients
+    (captured before the all-reduce) summed and scaled by 1/2 — the DataParallel
+    loss.mean() semantics of methods/DAF/DAF_train.py:341-342 / :397;
+  * rank 1 runs a target image of a different size, so its forward takes the unbatched
+    branch (tlod.da.daf) and finishes gradients in a different order than rank 0: the
+    static bucket order must keep the collectives paired.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "transfer-learning-library-for-object-detection_amd")
+H, W = 192, 320
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(rank, step, dev):
+    from tlod.detector.train import SyntheticCityscapes
+    b = list(SyntheticCityscapes(dev, H=H, W=W, G=4, pool=1, seed=50 + 10 * rank + step).next())
+    if rank == 1:  # smaller target image: the unbatched forward branch
+        t = SyntheticCityscapes(dev, H=H - 32, W=W, G=4, pool=1, seed=99 + step).next()
+        b[5], b[6] = t[5], t[6]
+    return tuple(b)
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    from tlod.detector.train import build_model, make_optimizer, train_step
+    from tlod.dist import GradBucketReducer
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = build_model("daf", dev, "vgg16", seed=rank)  # rank 1's init is overwritten by rank 0's
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    opt = make_optimizer(m, 2e-3, clip=10.0)
+    red = GradBucketReducer(m, bucket_mb=16.0)
+    names = {p: k for k, p in m.named_parameters()}
+    local = {}
+    red.arena.listeners.insert(0, lambda p: local.__setitem__(names[p], p.grad.detach().clone()))
+    rec = {"w0": {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}}
+    for step in range(2):
+        local.clear()
+        train_step(m, opt, _batch(rank, step, dev), reducer=red)
+        torch.cuda.synchronize()
+        rec[f"g{step}"] = {k: v.cpu() for k, v in local.items()}
+        rec[f"w{step + 1}"] = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    torch.save(rec, os.path.join(outdir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_daf_vgg16_data_parallel_two_ranks(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for step in (1, 2):
+        for k in r0[f"w{step}"]:
+            assert torch.equal(r0[f"w{step}"][k], r1[f"w{step}"][k]), (step, k)
+    # single-process reference: rank 0's initial weights, FusedSGDClip on (g0 + g1) / 2
+    sys.path.insert(0, PKG)
+    from tlod.detector.train import build_model, make_optimizer
+    dev = torch.device("cuda", 0)
+    m = build_model("daf", dev, "vgg16", seed=0)
+    m.load_state_dict({k: v.to(dev) for k, v in r0["w0"].items()}, strict=True)
+    opt = make_optimizer(m, 2e-3, clip=10.0)
+    for step in range(2):
+        opt.zero_grad()
+        n = 0
+        for k, p in m.named_parameters():
+            if k in r0[f"g{step}"]:
+                assert k in r1[f"g{step}"], k
+                p.grad = (r0[f"g{step}"][k].to(dev) + r1[f"g{step}"][k].to(dev)).contiguous()
+                n += 1
+        assert n == len(r0[f"g{step}"]) == len([p for p in m.parameters() if p.requires_grad])
+        opt.step(grad_scale=0.5)
+        torch.cuda.synchronize()
+        for k, p in m.named_parameters():
+            ref = p.detach().cpu()
+            assert torch.equal(ref, r0[f"w{step + 1}"][k]), (step, k,
+                                                              (ref - r0[f"w{step + 1}"][k]).abs().max())

@@ -110,3 +110,33 @@ def test_relu_dropout_fused():
     # same seed, same mask; another seed, another mask
     assert torch.equal(ReluDropoutFunction.apply(y, 0.5, 123), out.detach())
     assert not torch.equal(ReluDropoutFunction.apply(y, 0.5, 124), out.detach())
+
+
+def test_relu_dropout_passes_nan_like_torch():
+    """NaN must reach the loss as NaN (torch.relu / nn.Dropout propagate it), and
+    the backward passes the gradient at a NaN output as torch's threshold_backward does."""
+    from tlod.linear import ReluDropoutFunction
+    y = torch.tensor([1.0, -1.0, float("nan"), 0.0, 2.0, float("nan"), -3.0, 4.0], device=dev)
+    yr = y.clone().requires_grad_(True)
+    out = ReluDropoutFunction.apply(yr, 0.0, 0)
+    ref = torch.relu(y)
+    assert torch.equal(torch.isnan(out), torch.isnan(ref))
+    ok = ~torch.isnan(ref)
+    assert torch.equal(out[ok], ref[ok])
+    dout = torch.arange(1.0, 9.0, device=dev)
+    out.backward(dout)
+    yt = y.clone().requires_grad_(True)
+    torch.relu(yt).backward(dout)
+    assert torch.equal(yr.grad, yt.grad)
+
+
+def test_relu_dropout_p0_leaves_cpu_rng_alone():
+    """no seed draw from torch's CPU generator when dropout is off."""
+    from tlod.linear import relu_dropout
+    d = torch.nn.Dropout(0.5).eval()
+    torch.manual_seed(5)
+    a = torch.rand(3)
+    torch.manual_seed(5)
+    relu_dropout(torch.randn(64, device=dev), d)
+    b = torch.rand(3)
+    assert torch.equal(a, b)

@@ -5,6 +5,8 @@
 // threshold_backward.  The keep mask comes from the counter-based RNG of common.h (seeded
 // per call by the host) and is never stored: the backward reads it back from the output,
 // out > 0  <=>  y > 0 and the element was kept (scale >= 1 never underflows y > 0).
+// NaN passes through both ways as in torch.relu / nn.Dropout (a diverging head must reach
+// the loss as NaN): the tests are written !(v <= 0), which is true for NaN.
 #include "common.h"
 #include "tlod.h"
 
@@ -18,7 +20,7 @@ __global__ void __launch_bounds__(256) relu_dropout_kernel(const float* __restri
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const float v = y[i];
     const bool keep = p <= 0.f || rng_unit(seed, 0x5eed, (unsigned long long)i) >= (double)p;
-    out[i] = (v > 0.f && keep) ? v * scale : 0.f;
+    out[i] = (keep && !(v <= 0.f)) ? v * scale : 0.f;
   }
 }
 
@@ -32,12 +34,12 @@ __global__ void __launch_bounds__(256) relu_dropout_bwd_kernel(const float* __re
   float4* g4 = reinterpret_cast<float4*>(g);
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     const float4 d = d4[i], o = o4[i];
-    g4[i] = make_float4(o.x > 0.f ? d.x * scale : 0.f, o.y > 0.f ? d.y * scale : 0.f,
-                        o.z > 0.f ? d.z * scale : 0.f, o.w > 0.f ? d.w * scale : 0.f);
+    g4[i] = make_float4(!(o.x <= 0.f) ? d.x * scale : 0.f, !(o.y <= 0.f) ? d.y * scale : 0.f,
+                        !(o.z <= 0.f) ? d.z * scale : 0.f, !(o.w <= 0.f) ? d.w * scale : 0.f);
   }
   for (long long i = n4 * 4 + blockIdx.x * 256ll + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
-    g[i] = out[i] > 0.f ? dout[i] * scale : 0.f;
+    g[i] = !(out[i] <= 0.f) ? dout[i] * scale : 0.f;
 }
 
 unsigned grid256(long long n) {

@@ -4,6 +4,7 @@
 // .norm() and a .item() host sync, then a second loop of p.grad.mul_) followed by
 // torch.optim.SGD (methods/DAF/DAF_train.py:406-408).  Three stream-ordered launches, no
 // host sync, deterministic (fixed-order reductions):
+//   0. (data parallel) g = grad_scale * G, G the all-reduced gradient sum (applied as read);
 //   1. per-chunk sum of squares of the gradients;
 //   2. one workgroup: total = sqrt(sum), scale = clip / max(total, clip);
 //   3. per chunk: g' = scale*g; d = g' + wd*p; buf = m*buf + d; p -= lr*buf.
@@ -22,7 +23,7 @@ __device__ __forceinline__ bool vec4_ok(const void* a, const void* b, const void
 }
 
 __global__ void __launch_bounds__(256) sgd_sumsq_kernel(const tlod_sgd_chunk* __restrict__ chunks,
-                                                        float* __restrict__ partials) {
+                                                        float gs, float* __restrict__ partials) {
   const tlod_sgd_chunk c = chunks[blockIdx.x];
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (vec4_ok(c.grad, c.grad, c.grad, c.count)) {
@@ -30,12 +31,13 @@ __global__ void __launch_bounds__(256) sgd_sumsq_kernel(const tlod_sgd_chunk* __
     const long long n4 = c.count / 4;
 #pragma unroll 4
     for (long long i = threadIdx.x; i < n4; i += 256) {
-      const float4 g = g4[i];
+      float4 g = g4[i];
+      g.x *= gs; g.y *= gs; g.z *= gs; g.w *= gs;
       s0 += g.x * g.x; s1 += g.y * g.y; s2 += g.z * g.z; s3 += g.w * g.w;
     }
   } else {
     for (long long i = threadIdx.x; i < c.count; i += 256) {
-      const float g = c.grad[i];
+      const float g = c.grad[i] * gs;
       s0 += g * g;
     }
   }
@@ -65,16 +67,16 @@ __global__ void __launch_bounds__(256) sgd_norm_kernel(const float* __restrict__
   }
 }
 
-__device__ __forceinline__ void sgd1(float g, float& p, float& b, float scale, float wd,
-                                     float lr, float momentum) {
-  const float d = g * scale + wd * p;
+__device__ __forceinline__ void sgd1(float g, float& p, float& b, float gs, float scale,
+                                     float wd, float lr, float momentum) {
+  const float d = (g * gs) * scale + wd * p;
   b = momentum * b + d;
   p = p - lr * b;
 }
 
 __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* __restrict__ chunks,
                                                          const float* __restrict__ norm_scale,
-                                                         float momentum) {
+                                                         float gs, float momentum) {
   const tlod_sgd_chunk c = chunks[blockIdx.x];
   const float scale = norm_scale[1];
   if (vec4_ok(c.grad, c.param, c.momentum_buf, c.count)) {
@@ -86,10 +88,10 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
     for (long long i = threadIdx.x; i < n4; i += 256) {
       const float4 g = g4[i];
       float4 p = p4[i], b = b4[i];
-      sgd1(g.x, p.x, b.x, scale, c.weight_decay, c.lr, momentum);
-      sgd1(g.y, p.y, b.y, scale, c.weight_decay, c.lr, momentum);
-      sgd1(g.z, p.z, b.z, scale, c.weight_decay, c.lr, momentum);
-      sgd1(g.w, p.w, b.w, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.x, p.x, b.x, gs, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.y, p.y, b.y, gs, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.z, p.z, b.z, gs, scale, c.weight_decay, c.lr, momentum);
+      sgd1(g.w, p.w, b.w, gs, scale, c.weight_decay, c.lr, momentum);
       b4[i] = b;
       p4[i] = p;
     }
@@ -97,7 +99,7 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
   }
   for (long long i = threadIdx.x; i < c.count; i += 256) {
     float p = c.param[i], b = c.momentum_buf[i];
-    sgd1(c.grad[i], p, b, scale, c.weight_decay, c.lr, momentum);
+    sgd1(c.grad[i], p, b, gs, scale, c.weight_decay, c.lr, momentum);
     c.momentum_buf[i] = b;
     c.param[i] = p;
   }
@@ -107,18 +109,18 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
 
 using namespace tlod;
 
-extern "C" int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float momentum,
-                                 float clip_norm, float* partials, float* norm_scale,
-                                 tlod_stream_t stream) {
+extern "C" int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float grad_scale,
+                                 float momentum, float clip_norm, float* partials,
+                                 float* norm_scale, tlod_stream_t stream) {
   TLOD_CHECK_ARG(n_chunks > 0 && chunks && partials && norm_scale, "bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(sgd_sumsq_kernel, dim3(n_chunks), dim3(256), 0, s, chunks, partials);
+  hipLaunchKernelGGL(sgd_sumsq_kernel, dim3(n_chunks), dim3(256), 0, s, chunks, grad_scale, partials);
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(sgd_norm_kernel, dim3(1), dim3(256), 0, s, partials, n_chunks, clip_norm,
                      norm_scale);
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(sgd_update_kernel, dim3(n_chunks), dim3(256), 0, s, chunks, norm_scale,
-                     momentum);
+                     grad_scale, momentum);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

@@ -84,7 +84,7 @@ SIGNATURES = {
     "tlod_conv_wgrad_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                     c_size_t, P]),
     "tlod_relu_bwd_bias_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, P]),
-    "tlod_sgd_clip_f32": (c_int, [P, c_int, c_float, c_float, P, P, P]),
+    "tlod_sgd_clip_f32": (c_int, [P, c_int, c_float, c_float, c_float, P, P, P]),
     "tlod_conv_fwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, P, c_size_t, P]),
     "tlod_relu_bwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, P]),
@@ -112,6 +112,8 @@ SIGNATURES = {
     "tlod_stem_conv7x7s2_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_image_blob_u8": (c_int, [P, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                                   c_int, c_int, c_int, P, P]),
     "tlod_space_to_depth_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_depth_to_space_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_relu_dropout_f32": (c_int, [P, P, ctypes.c_longlong, c_float, c_uint64, P]),

@@ -121,10 +121,20 @@ RES101_YML = {"TRAIN": {"HAS_RPN": True, "BBOX_NORMALIZE_TARGETS_PRECOMPUTED": T
               "CROP_RESIZE_WITH_MAX_POOL": False}
 
 
-def setup_training_cfg(net="vgg16"):
-    """What DAF_train.py:168-204 does for --dataset cityscape --net vgg16|res101."""
+# per-dataset set_cfgs of the training drivers (methods/faster_rcnn/faster_rcnn_train.py:
+# 155-175, methods/DAF/DAF_train.py:168-198)
+DATASET_CFGS = {
+    "pascal_voc": ["ANCHOR_SCALES", "[8, 16, 32]", "ANCHOR_RATIOS", "[0.5,1,2]",
+                   "MAX_NUM_GT_BOXES", "20"],
+    "cityscape": ["ANCHOR_SCALES", "[4,8,16,32]", "ANCHOR_RATIOS", "[0.5,1,2]",
+                  "MAX_NUM_GT_BOXES", "50"],
+}
+
+
+def setup_training_cfg(net="vgg16", dataset="cityscape"):
+    """What the drivers do for --net vgg16|res101 --dataset cityscape|pascal_voc: cfgs/<net>.yml
+    then the dataset's set_cfgs."""
     reset_cfg()
     _merge(copy.deepcopy(VGG16_YML if net == "vgg16" else RES101_YML), cfg)
-    cfg_from_list(["ANCHOR_SCALES", "[4,8,16,32]", "ANCHOR_RATIOS", "[0.5,1,2]",
-                   "MAX_NUM_GT_BOXES", "50"])
+    cfg_from_list(DATASET_CFGS[dataset])
     return cfg

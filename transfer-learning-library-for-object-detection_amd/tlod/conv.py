@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .grads import grad_out
 
 
 # Optional launch timing (bench.py): list of (start_event, end_event, flops, kind, shape)
@@ -254,12 +255,15 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None):
     return dw
 
 
-def relu_bwd_bias(dy, y=None, want_db=True):
-    """g = dy * (y > 0) (y None: g = dy); db = sum_{n,h,w} g."""
+def relu_bwd_bias(dy, y=None, want_db=True, db_out=None):
+    """g = dy * (y > 0) (y None: g = dy); db = sum_{n,h,w} g (into db_out when given)."""
     dy = dy.contiguous()
     N, C, H, W = dy.shape
     g = torch.empty_like(dy) if y is not None else dy
-    db = torch.empty(C, dtype=torch.float32, device=dy.device) if want_db else None
+    db = None
+    if want_db:
+        db = db_out if db_out is not None else torch.empty(C, dtype=torch.float32,
+                                                           device=dy.device)
     _lib.check(_lib.lib().tlod_relu_bwd_bias_f32(_lib.ptr(dy), _lib.ptr(y.contiguous() if y is not None else None),
                                                  _lib.ptr(g), _lib.ptr(db), N, C, H * W,
                                                  _lib.stream_of(dy)), "relu_bwd_bias")
@@ -272,6 +276,7 @@ class ConvFunction(torch.autograd.Function):
         y = conv_fwd(x, weight, bias, relu)
         ctx.relu = bool(relu)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)  # gradient slots (tlod.grads)
         ctx.save_for_backward(x, weight, y if relu else None)
         return y
 
@@ -280,9 +285,10 @@ class ConvFunction(torch.autograd.Function):
         x, weight, y = ctx.saved_tensors
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], \
             ctx.has_bias and ctx.needs_input_grad[2]
-        g, db = relu_bwd_bias(dy, y if ctx.relu else None, want_db=need_b)
+        g, db = relu_bwd_bias(dy, y if ctx.relu else None, want_db=need_b,
+                              db_out=grad_out(ctx.params[1]) if need_b else None)
         dx = conv_dgrad(g, weight) if need_x else None
-        dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
+        dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0])) if need_w else None
         return dx, dw, db, None
 
 
@@ -308,6 +314,7 @@ class ConvBNFunction(torch.autograd.Function):
         y = conv_fwd(x, weight, shift, relu, scale=scale, residual=residual)
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
+        ctx.wparam = weight
         ctx.save_for_backward(x, weight, scale, y if relu else None)
         return y
 
@@ -318,7 +325,7 @@ class ConvBNFunction(torch.autograd.Function):
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         g, g_raw = relu_bwd_ex(dy, y if ctx.relu else None, scale, want_raw=need_res)
         dx = conv_dgrad(g, weight) if need_x else None
-        dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
+        dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.wparam)) if need_w else None
         return dx, dw, None, None, g_raw, None
 
 
@@ -332,13 +339,16 @@ def maxpool2x2(x):
     return y
 
 
-def maxpool_relu_bwd(dp, y, want_db=True):
+def maxpool_relu_bwd(dp, y, want_db=True, db_out=None):
     """Gradient through max_pool2d(2, 2) and the ReLU whose output y the pool read:
-    g = dp routed to each window's argmax where y > 0; db = sum g."""
+    g = dp routed to each window's argmax where y > 0; db = sum g (into db_out if given)."""
     dp = dp.contiguous()
     N, C, H, W = y.shape
     g = torch.empty_like(y)
-    db = torch.empty(C, dtype=torch.float32, device=y.device) if want_db else None
+    db = None
+    if want_db:
+        db = db_out if db_out is not None else torch.empty(C, dtype=torch.float32,
+                                                           device=y.device)
     _lib.check(_lib.lib().tlod_maxpool2x2_relu_bwd_f32(_lib.ptr(dp), _lib.ptr(y), N, C, H, W,
                                                        _lib.ptr(g), _lib.ptr(db),
                                                        _lib.stream_of(y)), "maxpool_relu_bwd")
@@ -376,6 +386,7 @@ class ConvPoolFunction(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         y = conv_fwd(x, weight, bias, True)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         ctx.save_for_backward(x, weight, y)
         return maxpool2x2(y)
 
@@ -384,9 +395,10 @@ class ConvPoolFunction(torch.autograd.Function):
         x, weight, y = ctx.saved_tensors
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
-        g, db = maxpool_relu_bwd(dp, y, want_db=need_b)
+        g, db = maxpool_relu_bwd(dp, y, want_db=need_b,
+                                 db_out=grad_out(ctx.params[1]) if need_b else None)
         dx = conv_dgrad(g, weight) if need_x else None
-        dw = conv_wgrad(g, x, weight.shape[2]) if need_w else None
+        dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0])) if need_w else None
         return dx, dw, db
 
 

@@ -13,25 +13,27 @@ import torch
 
 from ..config import cfg, setup_training_cfg
 
-CITYSCAPES_CLASSES = ("__background__", "bus", "bicycle", "car", "motorcycle", "person",
-                      "rider", "train", "truck")  # lib/datasets/cityscape.py:51-54
+from ..data.imdb import CITYSCAPE_CLASSES as CITYSCAPES_CLASSES  # cityscape.py:51-54
 
 
-METHODS = ("daf", "maf", "atf")
+METHODS = ("faster_rcnn", "daf", "maf", "atf")
 
 
-def build_model(method, device, net="vgg16", classes=CITYSCAPES_CLASSES, seed=0):
+def build_model(method, device, net="vgg16", classes=CITYSCAPES_CLASSES, seed=0,
+                dataset="cityscape"):
     """<method>.<net>(classes).create_architecture() (methods/<M>/<M>_train.py), random
-    init (the pretrained caffe weights are external downloads)."""
+    init (the pretrained caffe weights are external downloads).  method "faster_rcnn" is
+    the source-only detector (lib/model/faster_rcnn, methods/faster_rcnn)."""
     if method not in METHODS:
         raise ValueError(f"unknown method {method!r} (have {METHODS})")
     if net not in ("vgg16", "res101"):
         raise ValueError(f"unknown backbone {net!r}")
     import importlib
-    mod = importlib.import_module(f"..da.{method}", __package__)
+    mod = importlib.import_module(".faster_rcnn" if method == "faster_rcnn" else f"..da.{method}",
+                                  __package__)
     if net == "res101" and not hasattr(mod, "resnet"):
         raise NotImplementedError(f"{method} with ResNet101")
-    setup_training_cfg(net)
+    setup_training_cfg(net, dataset)
     torch.manual_seed(seed)
     if net == "vgg16":
         m = mod.vgg16(classes, pretrained=False, class_agnostic=False)
@@ -137,18 +139,21 @@ def default_clip(model):
 def train_step(model, optimizer, batch, lamda=0.1, clip=None, reducer=None):
     """One DAF/MAF/ATF iteration (the method's own loss sum, model.total_loss); returns the
     loss as a device tensor (no host sync)."""
+    from ..optim import FusedSGDClip
+    fused = isinstance(optimizer, FusedSGDClip)
     if reducer is not None:
-        reducer.zero_grad()  # grads are views into the reducer's flat buckets
+        reducer.zero_grad()  # grads are views into the arena the reducer all-reduces
     else:
         optimizer.zero_grad(set_to_none=True)
     out = model(*batch)
     loss = model.total_loss(out, lamda)
     loss.backward()
+    scale = 1.0
     if reducer is not None:
-        reducer.finish()
-    from ..optim import FusedSGDClip
-    if isinstance(optimizer, FusedSGDClip):
-        optimizer.step()  # clip_gradient + SGD fused
+        reducer.finish(scale=not fused)  # SUM all-reduce; the fused step applies 1/world
+        scale = reducer.grad_scale
+    if fused:
+        optimizer.step(grad_scale=scale)  # clip_gradient + SGD fused
     else:
         clip = default_clip(model) if clip is None else clip
         if clip:

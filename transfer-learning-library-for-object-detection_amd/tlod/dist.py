@@ -4,26 +4,31 @@ Replaces the reference's single-process ``nn.DataParallel`` (methods/DAF/DAF_tra
 341-342), which at ``--bs 1`` never runs more than one replica and reduces gradients to
 GPU 0 through the host thread.  Here:
 
-  * parameters are broadcast from rank 0 once at start;
-  * large parameters (>= ``direct_numel`` elements: the conv and fc weights, 98% of the
-    568 MB) are all-reduced in place as single messages from their post-accumulate-grad
-    hook, on the gradient tensor autograd produced (set_to_none: no zero fill, no
-    accumulate-add, no copy into a bucket);
-  * the small ones (biases, the narrow heads) have ``.grad`` views into flat buckets so
-    they travel in few messages; a hook counts ready parameters per bucket and launches
-    the bucket's async all-reduce when it is complete;
-  * every all-reduce is async (ReduceOp.AVG on RCCL — the DataParallel loss.mean()
-    semantics) and overlaps the rest of the backward (fc6/fc7 are ready first: the heads
-    backprop before the backbone);
-  * ``finish()`` waits for the outstanding buckets before clip_gradient / SGD, which
-    then run on identical gradients on every rank (no extra collective for the norm).
-
-Bucket sizing targets point-to-point xGMI rings: few, large messages (default 64 MB).
+  * parameters and buffers are broadcast from rank 0 once at start;
+  * every trainable gradient lives in the persistent arena (tlod.grads.GradArena), cut
+    into contiguous buckets (default 32 MB; a larger tensor — fc6's 411 MB — is a bucket
+    of its own); the all-reduce runs in place on the arena, no bucket copies;
+  * the buckets form ONE static list, identical on every rank, and are launched strictly
+    in that order: a gradient hook only marks its parameter ready, then the longest ready
+    prefix of the list is launched (async).  Ranks whose graphs finish gradients in a
+    different order (e.g. one rank batches source + target through one backbone pass and
+    another does not, tlod.da.daf) still issue the same collectives in the same order;
+  * the list order is the reverse parameter registration order for the first step; at the
+    end of the first step rank 0's observed gradient-ready order is broadcast and the
+    arena is re-laid out in it (once), so later steps launch each bucket as soon as its
+    last gradient lands;
+  * the reduction is SUM on every backend (the gloo tests run the production path); the
+    1/world of DataParallel's ``loss.mean()`` semantics is applied by the fused optimizer
+    as it reads the gradients (``grad_scale``), or by ``finish(scale=True)`` in place;
+  * ``finish()`` waits for every bucket before clip_gradient / SGD, which then run on
+    identical gradients on every rank (no extra collective for the norm).
 """
 import os
 
 import torch
 import torch.distributed as dist
+
+from .grads import GradArena, arena_of
 
 
 def init_from_env(backend=None):
@@ -45,84 +50,114 @@ def init_from_env(backend=None):
 
 
 class GradBucketReducer:
-    def __init__(self, model, bucket_mb=64.0, group=None, direct_numel=1 << 20):
+    def __init__(self, model, bucket_mb=32.0, group=None, relayout=True, arena=None):
         self.group = group
         self.world = dist.get_world_size(group)
-        self.params = [p for p in model.parameters() if p.requires_grad]
-        self.direct = {p for p in self.params if p.numel() >= direct_numel}
-        self.direct_work = []
-        backend = dist.get_backend(group)
-        self.avg = backend == "nccl"
-        # broadcast initial weights (and buffers) from rank 0
+        self.rank = dist.get_rank(group)
+        self.grad_scale = 1.0 / self.world
+        params = [p for p in model.parameters() if p.requires_grad]
         with torch.no_grad():
             for t in list(model.parameters()) + list(model.buffers()):
-                dist.broadcast(t.data, 0, group=group)
-        # buckets in reverse registration order (~ gradient readiness order)
-        cap = int(bucket_mb * 1024 * 1024 / 4)
-        buckets, cur, cur_n = [], [], 0
-        for p in reversed([q for q in self.params if q not in self.direct]):
-            if cur and cur_n + p.numel() > cap:
-                buckets.append(cur)
-                cur, cur_n = [], 0
+                dist.broadcast(t.data, dist.get_global_rank(group, 0) if group else 0,
+                               group=group)
+        if arena is None:
+            arena = arena_of(params[0]) if params else None
+            if arena is None or set(arena.params) != set(params):
+                n = len(params)
+                arena = GradArena(params, order=range(n - 1, -1, -1))
+        self.arena = arena
+        self.cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        self.relayout_pending = relayout
+        self.seen = []  # rank-local gradient-ready order of this step (parameter indices)
+        self._build_buckets()
+        arena.listeners.append(self._on_grad)
+
+    # ------------------------------------------------------------------ layout
+    def _build_buckets(self):
+        a = self.arena
+        self.buckets, self.bucket_of = [], {}
+        cur, start, end = [], None, None
+        for p in a.order:
+            off, n = a.span(p)
+            if cur and (off + n - start) > self.cap:
+                self.buckets.append({"params": cur, "lo": start, "hi": end})
+                cur = []
+            if not cur:
+                start = off
             cur.append(p)
-            cur_n += p.numel()
+            end = off + n
         if cur:
-            buckets.append(cur)
-        self.buckets = []
-        self.bucket_of = {}
-        for bi, ps in enumerate(buckets):
-            n = sum(p.numel() for p in ps)
-            flat = torch.zeros(n, dtype=ps[0].dtype, device=ps[0].device)
-            off = 0
-            for p in ps:
-                p.grad = flat[off:off + p.numel()].view_as(p)
+            self.buckets.append({"params": cur, "lo": start, "hi": end})
+        for bi, b in enumerate(self.buckets):
+            for p in b["params"]:
                 self.bucket_of[p] = bi
-                off += p.numel()
-            self.buckets.append({"flat": flat, "params": ps, "ready": 0, "work": None})
-        self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._reset()
 
-    def zero_grad(self):
+    def _reset(self):
         for b in self.buckets:
-            b["flat"].zero_()
-            b["ready"] = 0
-            b["work"] = None
-        for p in self.direct:
-            p.grad = None
-        self.direct_work = []
+            b["ready"], b["work"] = 0, None
+        self.next = 0  # first bucket of the static list not yet launched
+        self.marked = set()
+        self.seen = []
 
-    def _launch(self, b):
-        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
-        b["work"] = dist.all_reduce(b["flat"], op=op, group=self.group, async_op=True)
+    # ------------------------------------------------------------------ step
+    def zero_grad(self):
+        self.arena.zero_grad()
+        self._reset()
+
+    def _flat(self, b):
+        return self.arena.flat[b["lo"]:b["hi"]]
+
+    def _launch_ready_prefix(self):
+        while self.next < len(self.buckets):
+            b = self.buckets[self.next]
+            if b["ready"] != len(b["params"]):
+                return
+            b["work"] = dist.all_reduce(self._flat(b), op=dist.ReduceOp.SUM, group=self.group,
+                                        async_op=True)
+            self.next += 1
 
     def _on_grad(self, p):
-        if p in self.direct:
-            op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
-            self.direct_work.append(
-                (p, dist.all_reduce(p.grad, op=op, group=self.group, async_op=True)))
-            return
+        if p in self.marked:
+            raise RuntimeError("GradBucketReducer: a parameter received its gradient twice in "
+                               "one step (gradient accumulation needs zero_grad() between "
+                               "steps)")
+        self.marked.add(p)
+        self.seen.append(self.arena.index[p])
         b = self.buckets[self.bucket_of[p]]
         b["ready"] += 1
-        if b["ready"] == len(b["params"]):
-            self._launch(b)
+        self._launch_ready_prefix()
 
-    def finish(self):
-        for b in self.buckets:
-            if b["work"] is None:
-                self._launch(b)
+    def finish(self, scale=False):
+        """Launch what is left (in list order) and wait.  A parameter that got no gradient
+        this step contributes zeros (its .grad stays None, as with set_to_none).
+        scale=True: divide the gradients by the world size here (for optimizers that take
+        no grad_scale)."""
+        for b in self.buckets[self.next:]:
+            for p in b["params"]:
+                if p not in self.marked:
+                    self.arena.view(p).zero_()
+            b["ready"] = len(b["params"])
+        self._launch_ready_prefix()
         for b in self.buckets:
             b["work"].wait()
-            if not self.avg:
-                b["flat"].div_(self.world)
-            b["work"] = None
-            b["ready"] = 0
-        for p, w in self.direct_work:
-            w.wait()
-            if not self.avg:
-                p.grad.div_(self.world)
-        if len(self.direct_work) != len(self.direct):
-            raise RuntimeError("GradBucketReducer: a large parameter received no gradient this "
-                               "step (every rank must all-reduce the same tensors)")
-        self.direct_work = []
-        # small grads must still alias the flat buffers (zero them with reducer.zero_grad())
-        for p in self.params:
-            assert p.grad is not None
+        seen = self.seen
+        if self.relayout_pending:
+            self._relayout(seen)
+        if scale:
+            self.arena.flat.mul_(self.grad_scale)
+        self._reset()
+        return seen
+
+    def _relayout(self, seen):
+        """Adopt rank 0's gradient-ready order of the first step (broadcast, so every rank
+        builds the same bucket list)."""
+        self.relayout_pending = False
+        n = len(self.arena.params)
+        order = seen + [i for i in range(n) if i not in set(seen)]
+        dev = self.arena.flat.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor(order, dtype=torch.int64, device=dev)
+        dist.broadcast(t, dist.get_global_rank(self.group, 0) if self.group else 0,
+                       group=self.group)
+        self.arena.layout(t.cpu().tolist())
+        self._build_buckets()

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from .grads import grad_out
 
 MATHS = ("bf16x6", "bf16x3")
 
@@ -56,6 +57,7 @@ class LinearFunction(torch.autograd.Function):
         y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math)          # x W^T (+ b)
         ctx.math = math
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)  # gradient slots (tlod.grads)
         ctx.save_for_backward(x, weight)
         return y
 
@@ -69,9 +71,11 @@ class LinearFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(dy, weight.detach(), R, I, O, 1, 0, None, ctx.math)  # dy W
         if ctx.needs_input_grad[1]:
-            dw = gemm(dy, x, O, I, R, 0, 0, None, ctx.math)                # dy^T x
+            dw = gemm(dy, x, O, I, R, 0, 0, None, ctx.math,                # dy^T x
+                      out=grad_out(ctx.params[0]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.sum(0)
+            slot = grad_out(ctx.params[1])
+            db = dy.sum(0) if slot is None else torch.sum(dy, 0, out=slot)
         return dx, dw, db, None
 
 
@@ -116,11 +120,12 @@ class ReluDropoutFunction(torch.autograd.Function):
 
 def relu_dropout(y, dropout):
     """dropout(relu(y)) with the nn.Dropout module's p and training mode (its RNG stream is
-    libtlod's counter-based one, seeded from torch's CPU generator: no device sync)."""
+    libtlod's counter-based one, seeded from torch's CPU generator: no device sync; no draw
+    at all when p == 0 or in eval mode, so the CPU generator's stream is left alone)."""
     p = float(dropout.p) if dropout.training else 0.0
     if not fused_act():
         return dropout(torch.relu(y))
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0.0 else 0
     return ReluDropoutFunction.apply(y, p, seed)
 
 

@@ -3,8 +3,9 @@
 Same update as ``clip_gradient(model, 10.)`` (lib/model/utils/net_utils.py:38-49) followed
 by ``torch.optim.SGD(params, momentum=0.9)`` with the reference's param groups
 (methods/DAF/DAF_train.py:311-325: biases lr*(DOUBLE_BIAS+1) and no weight decay unless
-BIAS_DECAY; weights lr and WEIGHT_DECAY) — three launches; the only host wait is the
-descriptor-table upload when the gradient buffers moved (see __init__).
+BIAS_DECAY; weights lr and WEIGHT_DECAY) — three launches, no host wait: the gradients
+live in the persistent arena (tlod.grads), so the descriptor table is built and uploaded
+once per (arena layout, set of parameters with a gradient, learning rates).
 """
 import os
 
@@ -12,6 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .grads import GradArena, arena_of
 
 CHUNK = 65536
 _DESC = np.dtype([("param", np.uint64), ("grad", np.uint64), ("buf", np.uint64),
@@ -34,17 +36,22 @@ class FusedSGDClip:
         n_chunks = sum((p.numel() + CHUNK - 1) // CHUNK for p in self.params)
         self.partials = torch.empty(n_chunks, dtype=torch.float32, device=dev)
         self.norm_scale = torch.zeros(2, dtype=torch.float32, device=dev)
-        # descriptor tables per gradient-pointer set (set_to_none=True re-allocates the grads
-        # every step, so the table is rebuilt most steps).  The upload is a blocking copy:
-        # the host then waits for the queued backward once per step, which measured faster
-        # than letting it run ahead (64.4 vs 63.0 img/s, DAF VGG16 600x1200, same box) —
-        # TLOD_SGD_ASYNC_UPLOAD=1 selects the non-blocking copy (pinned buffers of torch's
-        # caching host allocator, reused only after their copy ran)
+        # gradient arena: reuse the one the parameters already belong to (e.g. the DP
+        # reducer's), else create one in registration order
+        a = arena_of(self.params[0])
+        if a is None or any(arena_of(p) is not a for p in self.params):
+            a = GradArena(self.params) if os.environ.get("TLOD_GRAD_ARENA", "1") != "0" else None
+        self.arena = a
+        # descriptor tables per gradient-pointer set; with the arena the key is stable and
+        # the (blocking, tiny) upload happens on the first step only
         self._tables = {}
         self._key = None
         self._n = 0
 
     def zero_grad(self, set_to_none=True):
+        if set_to_none and self.arena is not None:
+            self.arena.zero_grad()
+            return
         for p in self.params:
             if set_to_none:
                 p.grad = None
@@ -81,7 +88,7 @@ class FusedSGDClip:
         if arr.nbytes:
             host = torch.empty(arr.nbytes, dtype=torch.uint8, pin_memory=True)
             host.numpy()[:] = arr.view(np.uint8)
-            table.copy_(host, non_blocking=os.environ.get("TLOD_SGD_ASYNC_UPLOAD") == "1")
+            table.copy_(host)
         if len(self._tables) >= 8:
             self._tables.pop(next(iter(self._tables)))
         self._tables[key] = (table, len(rows))
@@ -89,11 +96,14 @@ class FusedSGDClip:
         return table
 
     @torch.no_grad()
-    def step(self):
+    def step(self, grad_scale=1.0):
+        """grad_scale: factor applied to every gradient as it is read (data parallel: 1/world
+        of the all-reduced sums, tlod.dist.GradBucketReducer.grad_scale)."""
         table = self._chunk_table()
         if self._n == 0:
             return self.norm_scale[0]
         _lib.check(_lib.lib().tlod_sgd_clip_f32(
-            _lib.ptr(table), self._n, self.momentum, self.clip_norm, _lib.ptr(self.partials),
-            _lib.ptr(self.norm_scale), _lib.stream_of(self.partials)), "sgd_clip")
+            _lib.ptr(table), self._n, float(grad_scale), self.momentum, self.clip_norm,
+            _lib.ptr(self.partials), _lib.ptr(self.norm_scale), _lib.stream_of(self.partials)),
+            "sgd_clip")
         return self.norm_scale[0]
