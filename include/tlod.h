@@ -366,6 +366,21 @@ int tlod_image_blob_u8(const uint8_t* src, int H, int W, const float* lut, const
                        const void* ytab, int Hr, int Wr, int y0, int x0, int Hd, int Wd, int Ho,
                        int Wo, float* out, tlod_stream_t stream);
 
+/* ------------------------------------------------------------------ Test-time detections
+ * Replaces: the per-class loop of the test drivers (methods/DAF/DAF_test.py:282-321): box
+ *   deltas * BBOX_NORMALIZE_STDS + MEANS, bbox_transform_inv + clip_boxes
+ *   (lib/model/rpn/bbox_transform.py:77-103, :125-133), / im_scale, then per class j >= 1
+ *   scores > score_thresh, descending sort, nms(TEST.NMS) (nms_cuda_kernel.cu semantics).
+ * rois (R, 5) of one image, cls_prob (R, C), bbox_pred (R, 4C) (or (R, 4) when
+ * class_agnostic); stds / means: 4 floats each in HOST memory; im_h, im_w: im_info[0:2].
+ * R <= 2048.  dets (C, R, 5) receives, for class j, counts[j] rows (x1, y1, x2, y2, score)
+ * in descending score order (ties: lower RoI index first); counts[0] = 0.  boxes_out
+ * (R, C, 4), optional (NULL to skip): every decoded, clipped, rescaled box. */
+int tlod_detect_f32(const float* rois, const float* cls_prob, const float* bbox_pred, int R,
+                    int C, int class_agnostic, const float* stds, const float* means, float im_h,
+                    float im_w, float im_scale, float score_thresh, float nms_thresh, float* dets,
+                    int32_t* counts, float* boxes_out, tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ MAF DRM
  * Replaces: the chunk / reshape / cat loops of DRM.forward, lib/MAF/drm.py:23-40 (a
  *   Python double loop over (H/s)*(W/s) chunks).  x: (B, C, H, W); the map is cropped

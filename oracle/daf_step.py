@@ -22,25 +22,89 @@ CFG = dict(pre_train=12000, post_train=2000, pre_test=6000, post_test=300, nms=0
            scales=(4, 8, 16, 32), ratios=(0.5, 1, 2), stride=16, pool=7, lamda=0.1)
 
 
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _t(a, like):
+    """numpy result of a restated op -> a tensor next to ``like`` (the oracle's torch parts
+    may run on the GPU: the reference's own fp32 arithmetic on this hardware)."""
+    return torch.from_numpy(np.ascontiguousarray(a)).to(like.device)
+
+
 class _RoIAlignAvgCPU(torch.autograd.Function):
     """float32 features: the CUDA kernels' arithmetic; float64 features (the exact-arithmetic
     reference of the gradient bars): the same sample geometry in double."""
 
     @staticmethod
     def forward(ctx, feat, rois):
-        f = feat.detach().numpy()
-        r = rois.detach().float().numpy()
-        ctx.meta = (r, f.shape, f.dtype)
+        f = _np(feat)
+        r = _np(rois.float())
+        ctx.meta = (r, f.shape, f.dtype, feat.device)
         if f.dtype == np.float64:
-            return torch.from_numpy(oroi.roi_align_avg_fwd64(f, r, CFG["pool"], CFG["pool"], 1 / 16))
-        return torch.from_numpy(oroi.roi_align_avg_fwd(f, r, CFG["pool"], CFG["pool"], 1 / 16))
+            return _t(oroi.roi_align_avg_fwd64(f, r, CFG["pool"], CFG["pool"], 1 / 16), feat)
+        return _t(oroi.roi_align_avg_fwd(f, r, CFG["pool"], CFG["pool"], 1 / 16), feat)
 
     @staticmethod
     def backward(ctx, g):
-        r, (B, C, H, W), dt = ctx.meta
+        r, (B, C, H, W), dt, _ = ctx.meta
         if dt == np.float64:
-            return torch.from_numpy(oroi.roi_align_avg_bwd64(g.numpy(), r, B, C, H, W, 1 / 16)), None
-        return torch.from_numpy(oroi.roi_align_avg_bwd(g.numpy(), r, B, C, H, W, 1 / 16)), None
+            return _t(oroi.roi_align_avg_bwd64(_np(g), r, B, C, H, W, 1 / 16), g), None
+        return _t(oroi.roi_align_avg_bwd(_np(g), r, B, C, H, W, 1 / 16), g), None
+
+
+def forced_relu(forced, site, x):
+    """ReLU, or — when ``forced`` holds masks for ``site`` — x * mask with the next mask of
+    that site: the fp64 gradient reference evaluated in the device's activation pattern
+    (a pre-activation within rounding of 0 may land on either side in two fp32 runs; the
+    gradient of the same piecewise-linear function needs the same side)."""
+    if forced and forced.get("__record__") is not None:  # record this run's own masks
+        forced["__record__"].setdefault(site, []).append((x > 0).detach())
+    lst = forced.get(site) if forced else None
+    if lst:
+        return x * lst.pop(0).to(device=x.device, dtype=x.dtype)
+    return F.relu(x)
+
+
+class SiteReLU(nn.Module):
+    def __init__(self, forced, site):
+        super().__init__()
+        self.forced, self.site = forced, site
+
+    def forward(self, x):
+        return forced_relu(self.forced, self.site, x)
+
+
+class SitePool(nn.Module):
+    """MaxPool2d(2, 2), or a gather at forced argmax indices (max_pool2d return_indices
+    layout) for the same reason."""
+
+    def __init__(self, forced, site):
+        super().__init__()
+        self.forced, self.site = forced, site
+
+    def forward(self, x):
+        if self.forced and self.forced.get("__record__") is not None:
+            self.forced["__record__"].setdefault(self.site, []).append(
+                F.max_pool2d(x.detach(), 2, 2, return_indices=True)[1])
+        lst = self.forced.get(self.site) if self.forced else None
+        if not lst:
+            return F.max_pool2d(x, 2, 2)
+        idx = lst.pop(0).to(x.device)
+        B, C, H, W = x.shape
+        return x.reshape(B, C, H * W).gather(2, idx.reshape(B, C, -1)).reshape(idx.shape)
+
+
+def vgg16_features(forced):
+    """torchvision vgg16().features[:-1] with named activation / pool sites."""
+    layers, cin = [], 3
+    for v in VGG16_CFG:
+        if v == "M":
+            layers.append(SitePool(forced, f"base.{len(layers)}"))
+        else:
+            layers += [nn.Conv2d(cin, v, 3, padding=1), SiteReLU(forced, f"base.{len(layers) + 1}")]
+            cin = v
+    return nn.Sequential(*layers)
 
 
 class _GRL(torch.autograd.Function):
@@ -73,20 +137,15 @@ class OracleDAF(nn.Module):
         super().__init__()
         self.backbone = backbone
         self.rcnn_cfg = dict(orpn.DEFAULT_RCNN)
+        self.forced = {}  # site -> masks / pool indices to use instead of recomputing them
         if backbone == "vgg16":
-            layers, cin = [], 3
-            for v in VGG16_CFG:
-                if v == "M":
-                    layers.append(nn.MaxPool2d(2, 2))
-                else:
-                    layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
-                    cin = v
-            self.RCNN_base = nn.Sequential(*layers)
+            self.RCNN_base = vgg16_features(self.forced)
             for i in range(10):
                 for p in self.RCNN_base[i].parameters():
                     p.requires_grad = False
-            self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), nn.ReLU(True), nn.Dropout(dropout),
-                                          nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout))
+            self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), SiteReLU(self.forced, "fc6"),
+                                          nn.Dropout(dropout), nn.Linear(4096, 4096),
+                                          SiteReLU(self.forced, "fc7"), nn.Dropout(dropout))
             din, dfeat = 512, 4096
             self.splits = (10, 16, 23)  # shared frozen prefix, conv3 end, conv4 end
         else:
@@ -113,7 +172,7 @@ class OracleDAF(nn.Module):
         self.base_anchors = orpn.make_base_anchors(CFG["scales"], CFG["ratios"])
 
     def _rpn(self, feat):
-        x = F.relu(self.RCNN_rpn.RPN_Conv(feat))
+        x = forced_relu(self.forced, "rpn", self.RCNN_rpn.RPN_Conv(feat))
         score = self.RCNN_rpn.RPN_cls_score(x)
         B, C, H, W = score.shape
         sr = score.view(B, 2, C * H // 2, W)
@@ -122,13 +181,13 @@ class OracleDAF(nn.Module):
 
     def _image_da(self, feat):
         x = _GRL.apply(feat, 0.1)
-        return self.RCNN_imageDA.Conv2(F.relu(self.RCNN_imageDA.Conv1(x)))
+        return self.RCNN_imageDA.Conv2(forced_relu(self.forced, "ida", self.RCNN_imageDA.Conv1(x)))
 
     def _instance_da(self, x):
         m = self.RCNN_instanceDA
         x = _GRL.apply(x, 0.1)
-        x = F.dropout(F.relu(m.dc_ip1(x)), self.dropout, self.training)
-        x = F.dropout(F.relu(m.dc_ip2(x)), self.dropout, self.training)
+        x = F.dropout(forced_relu(self.forced, "ip1", m.dc_ip1(x)), self.dropout, self.training)
+        x = F.dropout(forced_relu(self.forced, "ip2", m.dc_ip2(x)), self.dropout, self.training)
         return torch.sigmoid(m.clssifer(x))
 
     def train(self, mode=True):
@@ -162,42 +221,45 @@ class OracleDAF(nn.Module):
         c3, c4, base = self._backbone(im)
         score, sr, prob, bbox = self._rpn(base)
         gt, info = gt.float(), info.float()  # the sampling ops see the reference's float32
-        rois = orpn.proposal_layer(prob.detach().float().numpy(), bbox.detach().float().numpy(), info.numpy(),
+        rois = orpn.proposal_layer(_np(prob.float()), _np(bbox.float()), _np(info),
                                    self.base_anchors, c["stride"], c["pre_train"], c["post_train"],
                                    c["nms"])
+        props = rois
         if rois_override is not None:
             rois = rois_override[0]
         H, W = score.shape[2:]
-        lab, tgt, iw, ow = orpn.anchor_target(H, W, gt.numpy(), info.numpy(), self.base_anchors,
+        lab, tgt, iw, ow = orpn.anchor_target(H, W, _np(gt), _np(info), self.base_anchors,
                                               c["stride"], rng)
-        lab_t = torch.from_numpy(lab).view(-1)
+        lab_t = _t(lab, bbox).view(-1)
         keep = lab_t != -1
         s2 = sr.permute(0, 2, 3, 1).contiguous().view(-1, 2)
         rpn_loss_cls = F.cross_entropy(s2[keep], lab_t[keep].long())
-        rpn_loss_box = _smooth_l1(bbox, torch.from_numpy(tgt), torch.from_numpy(iw),
-                                  torch.from_numpy(ow), sigma=3, dim=[1, 2, 3])
-        r, rl, rt, riw, row = orpn.proposal_target(rois, gt.numpy(), rng, self.rcnn_cfg)
-        rl = torch.from_numpy(rl).view(-1).long()
-        pooled = _RoIAlignAvgCPU.apply(base, torch.from_numpy(r).view(-1, 5))
+        rpn_loss_box = _smooth_l1(bbox, _t(tgt, bbox), _t(iw, bbox),
+                                  _t(ow, bbox), sigma=3, dim=[1, 2, 3])
+        r, rl, rt, riw, row = orpn.proposal_target(rois, _np(gt), rng, self.rcnn_cfg)
+        rl = _t(rl, bbox).view(-1).long()
+        pooled = _RoIAlignAvgCPU.apply(base, _t(r, base).view(-1, 5))
         fc7 = self._head_to_tail(pooled)
         bp = self.RCNN_bbox_pred(fc7).view(fc7.size(0), -1, 4)
         bp = torch.gather(bp, 1, rl.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
         cls = self.RCNN_cls_score(fc7)
         rcnn_cls = F.cross_entropy(cls, rl)
-        rcnn_box = _smooth_l1(bp, torch.from_numpy(rt).view(-1, 4), torch.from_numpy(riw).view(-1, 4),
-                              torch.from_numpy(row).view(-1, 4))
+        rcnn_box = _smooth_l1(bp, _t(rt, bp).view(-1, 4), _t(riw, bp).view(-1, 4),
+                              _t(row, bp).view(-1, 4))
         # target image: RPN in eval mode (TEST proposals)
         t_c3, t_c4, t_base = self._backbone(t_im)
         _, _, t_prob, t_bbox = self._rpn(t_base)
-        t_rois = orpn.proposal_layer(t_prob.detach().float().numpy(), t_bbox.detach().float().numpy(),
-                                     t_info.float().numpy(), self.base_anchors, c["stride"], c["pre_test"],
+        t_rois = orpn.proposal_layer(t__np(prob.float()), t__np(bbox.float()),
+                                     _np(t_info.float()), self.base_anchors, c["stride"], c["pre_test"],
                                      c["post_test"], c["nms"])
+        t_props = t_rois
         if rois_override is not None:
             t_rois = rois_override[1]
-        t_pooled = _RoIAlignAvgCPU.apply(t_base, torch.from_numpy(t_rois).view(-1, 5))
+        t_pooled = _RoIAlignAvgCPU.apply(t_base, _t(t_rois, t_base).view(-1, 5))
         t_fc7 = self._head_to_tail(t_pooled)
         return dict(rpn_loss_cls=rpn_loss_cls, rpn_loss_box=rpn_loss_box, RCNN_loss_cls=rcnn_cls,
-                    RCNN_loss_bbox=rcnn_box, rois=r, c3=c3, c4=c4, base=base, fc7=fc7, cls=cls,
+                    RCNN_loss_bbox=rcnn_box, rois=r, props=props, t_props=t_props, c3=c3, c4=c4,
+                    base=base, fc7=fc7, cls=cls,
                     t_c3=t_c3, t_c4=t_c4, t_base=t_base, t_fc7=t_fc7)
 
     def forward(self, batch, rng, rois_override=None):
@@ -205,13 +267,15 @@ class OracleDAF(nn.Module):
         base, fc7, t_base, t_fc7 = d["base"], d["fc7"], d["t_base"], d["t_fc7"]
         # DA (faster_rcnn.py:181-220)
         bs = self._image_da(base)
-        da_img = F.nll_loss(F.log_softmax(bs, 1), torch.ones(bs.shape[0], *bs.shape[2:], dtype=torch.long))
+        da_img = F.nll_loss(F.log_softmax(bs, 1), torch.ones(bs.shape[0], *bs.shape[2:], dtype=torch.long,
+                                                             device=bs.device))
         ins = self._instance_da(fc7)
         da_ins = F.binary_cross_entropy(ins, torch.ones_like(ins))
         cst = F.softmax(bs, 1)[:, 1].mean().detach()
         da_cst = ((ins - cst) ** 2).sum()
         tbs = self._image_da(t_base)
-        t_da_img = F.nll_loss(F.log_softmax(tbs, 1), torch.zeros(tbs.shape[0], *tbs.shape[2:], dtype=torch.long))
+        t_da_img = F.nll_loss(F.log_softmax(tbs, 1), torch.zeros(tbs.shape[0], *tbs.shape[2:],
+                                                                dtype=torch.long, device=tbs.device))
         t_ins = self._instance_da(t_fc7)
         y = torch.ones_like(t_ins)
         y[:256] = 0  # InstanceLabelResizeLayer quirk (LabelResizeLayer.py:48-55)

@@ -13,7 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import rpn as orpn
-from .daf_step import VGG16_CFG, _RoIAlignAvgCPU, _smooth_l1
+from .daf_step import SiteReLU, _np, _RoIAlignAvgCPU, _smooth_l1, _t, forced_relu, vgg16_features
 
 
 class OracleFRCNN(nn.Module):
@@ -23,20 +23,15 @@ class OracleFRCNN(nn.Module):
         self.backbone = backbone
         self.rcnn_cfg = dict(orpn.DEFAULT_RCNN)
         A = len(scales) * len(ratios)
+        self.forced = {}  # site -> forced masks / pool indices (oracle.daf_step.forced_relu)
         if backbone == "vgg16":
-            layers, cin = [], 3
-            for v in VGG16_CFG:
-                if v == "M":
-                    layers.append(nn.MaxPool2d(2, 2))
-                else:
-                    layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
-                    cin = v
-            self.RCNN_base = nn.Sequential(*layers)
+            self.RCNN_base = vgg16_features(self.forced)
             for i in range(10):
                 for p in self.RCNN_base[i].parameters():
                     p.requires_grad = False
-            self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), nn.ReLU(True), nn.Dropout(dropout),
-                                          nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout))
+            self.RCNN_top = nn.Sequential(nn.Linear(25088, 4096), SiteReLU(self.forced, "fc6"),
+                                          nn.Dropout(dropout), nn.Linear(4096, 4096),
+                                          SiteReLU(self.forced, "fc7"), nn.Dropout(dropout))
             din, dfeat = 512, 4096
         else:
             from .resnet import resnet101_parts
@@ -69,7 +64,7 @@ class OracleFRCNN(nn.Module):
         """Training-mode losses (faster_rcnn.py:39-115).  rois_override: the device run's
         proposals (the score sort of near-tied random-init scores is order-sensitive)."""
         base = self.RCNN_base(im)
-        x = F.relu(self.RCNN_rpn.RPN_Conv(base))
+        x = forced_relu(self.forced, "rpn", self.RCNN_rpn.RPN_Conv(base))
         score = self.RCNN_rpn.RPN_cls_score(x)
         B, C, H, W = score.shape
         sr = score.view(B, 2, C * H // 2, W)
@@ -77,29 +72,29 @@ class OracleFRCNN(nn.Module):
         bbox = self.RCNN_rpn.RPN_bbox_pred(x)
         pre, post = self.pre_post_train
         gt, info = gt.float(), info.float()  # the sampling ops see the reference's float32
-        rois = orpn.proposal_layer(prob.detach().float().numpy(), bbox.detach().float().numpy(),
-                                   info.numpy(),
+        rois = orpn.proposal_layer(_np(prob.float()), _np(bbox.float()),
+                                   _np(info),
                                    self.base_anchors, 16, pre, post, 0.7)
         if rois_override is not None:
             rois = rois_override
-        lab, tgt, iw, ow = orpn.anchor_target(H, W, gt.numpy(), info.numpy(), self.base_anchors,
+        lab, tgt, iw, ow = orpn.anchor_target(H, W, _np(gt), _np(info), self.base_anchors,
                                               16, rng)
-        lab_t = torch.from_numpy(lab).view(-1)
+        lab_t = _t(lab, bbox).view(-1)
         keep = lab_t != -1
         s2 = sr.permute(0, 2, 3, 1).contiguous().view(-1, 2)
         rpn_loss_cls = F.cross_entropy(s2[keep], lab_t[keep].long())
-        rpn_loss_box = _smooth_l1(bbox, torch.from_numpy(tgt), torch.from_numpy(iw),
-                                  torch.from_numpy(ow), sigma=3, dim=[1, 2, 3])
-        r, rl, rt, riw, row = orpn.proposal_target(rois, gt.numpy(), rng, self.rcnn_cfg)
-        rl = torch.from_numpy(rl).view(-1).long()
-        pooled = _RoIAlignAvgCPU.apply(base, torch.from_numpy(r).view(-1, 5))
+        rpn_loss_box = _smooth_l1(bbox, _t(tgt, bbox), _t(iw, bbox),
+                                  _t(ow, bbox), sigma=3, dim=[1, 2, 3])
+        r, rl, rt, riw, row = orpn.proposal_target(rois, _np(gt), rng, self.rcnn_cfg)
+        rl = _t(rl, bbox).view(-1).long()
+        pooled = _RoIAlignAvgCPU.apply(base, _t(r, base).view(-1, 5))
         fc7 = self._head_to_tail(pooled)
         bp = self.RCNN_bbox_pred(fc7).view(fc7.size(0), -1, 4)
         bp = torch.gather(bp, 1, rl.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1)
         cls = self.RCNN_cls_score(fc7)
         rcnn_cls = F.cross_entropy(cls, rl)
-        rcnn_box = _smooth_l1(bp, torch.from_numpy(rt).view(-1, 4),
-                              torch.from_numpy(riw).view(-1, 4), torch.from_numpy(row).view(-1, 4))
+        rcnn_box = _smooth_l1(bp, _t(rt, bp).view(-1, 4),
+                              _t(riw, bp).view(-1, 4), _t(row, bp).view(-1, 4))
         return dict(rpn_loss_cls=rpn_loss_cls, rpn_loss_box=rpn_loss_box, RCNN_loss_cls=rcnn_cls,
                     RCNN_loss_bbox=rcnn_box, rois=r, labels=rl)
 
@@ -108,7 +103,7 @@ class OracleFRCNN(nn.Module):
         """Eval-mode head on given rois (faster_rcnn.py:70-113 with training False):
         (cls_prob (R, C), bbox_pred (R, 4C))."""
         base = self.RCNN_base(im)
-        pooled = _RoIAlignAvgCPU.apply(base, torch.from_numpy(np.asarray(rois)).view(-1, 5))
+        pooled = _RoIAlignAvgCPU.apply(base, _t(np.asarray(rois), base).view(-1, 5))
         fc7 = self._head_to_tail(pooled)
         return F.softmax(self.RCNN_cls_score(fc7), 1), self.RCNN_bbox_pred(fc7)
 

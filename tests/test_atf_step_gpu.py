@@ -17,14 +17,20 @@ IDX = [3, 4, 5, 6, 8, 9, 10, 11]
 VIEWS = ("conv3_s.", "conv3_t.", "conv34_s.", "conv34_t.", "conv45_s.", "conv45_t.", "RCNN_rpn_t.")
 
 
-@pytest.mark.parametrize("net,H,W,seed", [("vgg16", 192, 320, 0), ("vgg16", 224, 288, 3),
-                                          ("res101", 224, 320, 5)])
-def test_atf_losses_and_grads_match_oracle(net, H, W, seed):
+@pytest.mark.parametrize("net,H,W,seed,ncls", [("vgg16", 192, 320, 0, 9), ("vgg16", 224, 288, 3, 9),
+                                               ("res101", 224, 320, 5, 9),
+                                               ("res101", 256, 320, 6, 21)])
+def test_atf_losses_and_grads_match_oracle(net, H, W, seed, ncls):
+    """ncls 21 with ResNet101 (RCNN batch 128, cfgs/res101.yml) is BASELINE config 5's
+    detector: ATF ResNet101 PASCAL -> Clipart, the 20 VOC classes + background."""
     from oracle.atf_step import OracleATF, total_loss
     from oracle.daf_step import synthetic_batch
     from tlod.config import cfg
     from tlod.detector.train import build_model
-    m = build_model("atf", dev, net=net, seed=seed)
+    from tlod.data.imdb import VOC_CLASSES
+    from tlod.detector.train import CITYSCAPES_CLASSES
+    classes = VOC_CLASSES if ncls == 21 else CITYSCAPES_CLASSES
+    m = build_model("atf", dev, net=net, seed=seed, classes=classes)
     with torch.no_grad():  # make the two branches differ
         for p in m.RCNN_base_t[m.splits[0]:].parameters():
             if p.requires_grad:
@@ -32,7 +38,10 @@ def test_atf_losses_and_grads_match_oracle(net, H, W, seed):
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
-    o = OracleATF(dropout=0.0, backbone=net).train()
+    o = OracleATF(n_classes=ncls, dropout=0.0, backbone=net).train()
+    assert m.RCNN_cls_score.out_features == ncls
+    if net == "res101":
+        assert o.rcnn_cfg["batch"] == 128 and cfg.TRAIN.BATCH_SIZE == 128
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items() if not k.startswith(VIEWS)}
     o.load_state_dict(sd, strict=True)
     assert cfg.TEST.RPN_POST_NMS_TOP_N == 300

@@ -6,13 +6,11 @@ random-init RPN scores is order-sensitive at the 1e-7 level); everything else â€
 backbone, RPN losses, anchor/proposal targets, RoIAlign, heads, DA losses â€” is computed
 independently by both sides.  Bar: every loss within 1e-4 relative (north star: 1e-3).
 """
-import copy
-
 import numpy as np
 import pytest
 import torch
 
-from helpers import assert_grad_bar, grad_errors
+from helpers import arm_device_taps, pattern_grad_bar, record_pattern
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -37,35 +35,73 @@ def _models(H, W, seed):
     return m, o, cpu_batch
 
 
-@pytest.mark.parametrize("H,W,seed", [(192, 320, 0), (256, 384, 1)])
+@pytest.mark.parametrize("H,W,seed", [(192, 320, 0), (256, 384, 1), (600, 1200, 2)])
 def test_daf_losses_and_grads_match_oracle(H, W, seed):
     m, o, cpu_batch = _models(H, W, seed)
     gpu_batch = tuple(t.to(dev) for t in cpu_batch)
     m.replay_rng = np.random.RandomState(3)
     m.capture = {}
+    taps = arm_device_taps(m)
     out = m(*gpu_batch)
     from tlod.detector.train import daf_loss
     loss = daf_loss(out)
     loss.backward()
-    ref = o(cpu_batch, np.random.RandomState(3),
-            rois_override=(m.capture["s_rois"].cpu().numpy(), m.capture["t_rois"].cpu().numpy()))
+    ov = (m.capture["s_rois"].cpu().numpy(), m.capture["t_rois"].cpu().numpy())
     from oracle.daf_step import total_loss
-    rl = total_loss(ref)
-    rl.backward()
+    box = {}
+
+    def run32():
+        box["ref"] = o(cpu_batch, np.random.RandomState(3), rois_override=ov)
+        total_loss(box["ref"]).backward()
+    own = record_pattern(o, run32)
+    ref = box["ref"]
     for name, i in zip(LOSSES, IDX):
         g, r = float(out[i].detach()), float(ref[name].detach())
         assert abs(g - r) <= 1e-4 * max(abs(r), 1e-3), (name, g, r)
     # sampled RoIs identical (replayed draws on identical proposals)
     np.testing.assert_array_equal(out[0].cpu().numpy().reshape(-1, 5), ref["rois"].reshape(-1, 5))
-    # gradients of every trainable parameter against an fp64 run of the same step (same
-    # weights, RoIs and draws): at most 2x the fp32 CPU oracle's own error
-    o64 = copy.deepcopy(o).double()
-    for p in o64.parameters():
-        p.grad = None
-    b64 = tuple(t.double() if t.is_floating_point() else t for t in cpu_batch)
-    r64 = o64(b64, np.random.RandomState(3),
-              rois_override=(m.capture["s_rois"].cpu().numpy(), m.capture["t_rois"].cpu().numpy()))
-    total_loss(r64).backward()
-    errs = grad_errors(m.named_parameters(), o, o64)
-    print({k: (f"{a:.2e}", f"{b:.2e}") for k, (a, b) in errs.items()})
-    assert_grad_bar(errs)
+    # gradients of every trainable parameter vs fp64 runs of the same step in matched
+    # activation patterns: at most 2x the error of the reference's own fp32 arithmetic
+    # (torch CPU, torch on this GPU) â€” VERDICT r1 2a, tests/helpers.pattern_grad_bar
+    pattern_grad_bar(m, o, lambda mod, b: total_loss(mod(b, np.random.RandomState(3),
+                                                         rois_override=ov)),
+                     cpu_batch, taps, out[7].numel(), own)
+
+
+def _iou(a, b):
+    """(n,4) x (m,4) IoU, +1 pixel convention."""
+    a, b = a.astype(np.float64), b.astype(np.float64)
+    iw = np.minimum(a[:, None, 2], b[None, :, 2]) - np.maximum(a[:, None, 0], b[None, :, 0]) + 1
+    ih = np.minimum(a[:, None, 3], b[None, :, 3]) - np.maximum(a[:, None, 1], b[None, :, 1]) + 1
+    inter = np.clip(iw, 0, None) * np.clip(ih, 0, None)
+    aa = (a[:, 2] - a[:, 0] + 1) * (a[:, 3] - a[:, 1] + 1)
+    ab = (b[:, 2] - b[:, 0] + 1) * (b[:, 3] - b[:, 1] + 1)
+    return inter / (aa[:, None] + ab[None, :] - inter)
+
+
+@pytest.mark.parametrize("H,W,seed", [(256, 384, 4), (600, 1200, 5)])
+def test_daf_proposals_without_override(H, W, seed):
+    """the device's own source (TRAIN 12000 -> 2000) and target (TEST 6000 ->
+    300) proposals against the oracle's own, from each side's RPN outputs (no override).
+    Near-tied random-init scores can reorder the sort and move the top-N boundary, so the
+    proposals are compared as sets: >= 99.5% of each side's boxes have an IoU >= 0.999
+    partner on the other side.  The RPN losses do not depend on the proposals: 1e-4."""
+    m, o, cpu_batch = _models(H, W, seed)
+    m.replay_rng = np.random.RandomState(3)
+    m.capture = {}
+    with torch.no_grad():
+        out = m(*tuple(t.to(dev) for t in cpu_batch))
+        ref = o._detect(cpu_batch, np.random.RandomState(3))
+    for name, i in (("rpn_loss_cls", 3), ("rpn_loss_box", 4)):
+        g, r = float(out[i]), float(ref[name])
+        assert abs(g - r) <= 1e-4 * max(abs(r), 1e-3), (name, g, r)
+    for key, ref_key in (("s_rois", "props"), ("t_rois", "t_props")):
+        d = m.capture[key].cpu().numpy().reshape(-1, 5)
+        r = ref[ref_key].reshape(-1, 5)
+        d = d[(d[:, 3] > d[:, 1]) | (d[:, 4] > d[:, 2])]  # drop the zero padding rows
+        r = r[(r[:, 3] > r[:, 1]) | (r[:, 4] > r[:, 2])]
+        assert abs(len(d) - len(r)) <= max(2, len(r) // 200), (key, len(d), len(r))
+        iou = _iou(d[:, 1:], r[:, 1:])
+        for side, best in (("device", iou.max(1)), ("oracle", iou.max(0))):
+            frac = float((best >= 0.999).mean())
+            assert frac >= 0.995, (key, side, frac)

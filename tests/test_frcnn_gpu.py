@@ -6,17 +6,15 @@ against the CPU oracle (oracle/blob.py, oracle/frcnn_step.py).
     roibatchLoader crop / pad / gt padding, the device image blob) equals the oracle's
     literal restatement bit for bit, item by item;
   * one training step from that VOC directory: every loss within 1e-4 of the oracle, the
-    sampled RoIs identical (replayed numpy draws), every gradient within 2x the fp32 CPU
-    oracle's own error against an fp64 run of the same step (tests/helpers.assert_grad_bar);
+    sampled RoIs identical (replayed numpy draws), every gradient within 2x the error of the
+    reference's own fp32 arithmetic (tests/helpers.pattern_grad_bar);
   * eval mode returns the TEST proposals and per-class outputs (faster_rcnn.py:62-115).
 """
-import copy
-
 import numpy as np
 import pytest
 import torch
 
-from helpers import assert_grad_bar, grad_errors
+from helpers import arm_device_taps, pattern_grad_bar, record_pattern
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -75,6 +73,7 @@ def test_source_only_vgg16_step_config1(tmp_path):
     assert tuple(data.shape) == (1, 3, 600, 1000)
     m.replay_rng = np.random.RandomState(3)
     m.capture = {}
+    taps = arm_device_taps(m)
     out = m(data, im_info, gt, num)
     loss = m.total_loss(out)
     loss.backward()
@@ -84,8 +83,13 @@ def test_source_only_vgg16_step_config1(tmp_path):
     o.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=True)
     cpu = (data.cpu(), im_info.cpu(), gt.cpu())
     s_rois = m.capture["s_rois"].cpu().numpy()
-    ref = o(*cpu, np.random.RandomState(3), rois_override=s_rois)
-    o_total(ref).backward()
+    box = {}
+
+    def run32():
+        box["ref"] = o(*cpu, np.random.RandomState(3), rois_override=s_rois)
+        o_total(box["ref"]).backward()
+    own = record_pattern(o, run32)
+    ref = box["ref"]
     names = ["rpn_loss_cls", "rpn_loss_box", "RCNN_loss_cls", "RCNN_loss_bbox"]
     for name, i in zip(names, [3, 4, 5, 6]):
         g, r = float(out[i].detach()), float(ref[name].detach())
@@ -93,14 +97,9 @@ def test_source_only_vgg16_step_config1(tmp_path):
     np.testing.assert_array_equal(out[0].cpu().numpy().reshape(-1, 5), ref["rois"].reshape(-1, 5))
     np.testing.assert_array_equal(out[7].cpu().numpy(), ref["labels"].numpy())
 
-    o64 = copy.deepcopy(o).double()
-    for p in o64.parameters():
-        p.grad = None
-    ref64 = o64(*(t.double() for t in cpu), np.random.RandomState(3), rois_override=s_rois)
-    o_total(ref64).backward()
-    errs = grad_errors(m.named_parameters(), o, o64)
-    print({k: (f"{a:.2e}", f"{b:.2e}") for k, (a, b) in errs.items()})
-    assert_grad_bar(errs)
+    pattern_grad_bar(m, o, lambda mod, b: o_total(mod(*b, np.random.RandomState(3),
+                                                      rois_override=s_rois)),
+                     cpu, taps, None, own)
 
     # and a full step (clip_gradient(10) + SGD) trains
     opt = make_optimizer(m, 1e-3)

@@ -165,3 +165,44 @@ def test_proposal_target_device_rng():
     assert 8 <= nfg <= 64            # every gt is itself a fg candidate
     assert (lab[nfg:] == 0).all()    # fg first, then bg
     assert np.all(iw.cpu().numpy()[0][lab > 0] == 1) and np.all(iw.cpu().numpy()[0][lab == 0] == 0)
+
+
+def test_device_subset_sampling_is_uniform():
+    """the production sampler (block_random_subset: per-candidate hashed
+    keys, radix-selected smallest k) picks every candidate with the same probability, as
+    the reference's np.random.permutation(n)[:k] does (anchor_target_layer.py:123-145).
+    Over 1200 seeds each fg / bg candidate's selection count stays within 5 sigma of the
+    binomial mean k/n."""
+    from tlod.rpn.anchor_target import anchor_target, rpn_cfg_struct
+    from tlod.config import setup_training_cfg
+    setup_training_cfg("vgg16")
+    H, W = 37, 75
+    rng = np.random.default_rng(21)
+    gts = gt_set(rng, G=50, W=W * 16, H=H * 16)[None]
+    gts[0, :, 2:4] = np.maximum(gts[0, :, 2:4], gts[0, :, 0:2] + 200)  # big boxes: many fg
+    gts[0, :, 2] = np.minimum(gts[0, :, 2], W * 16 - 1)
+    gts[0, :, 3] = np.minimum(gts[0, :, 3], H * 16 - 1)
+    im_info = np.array([[H * 16, W * 16, 1.0]], np.float32)
+    ident = type("N", (), {"permutation": lambda self, n: np.arange(n)})()
+    full = orpn.anchor_target(H, W, gts, im_info, BASE, 16, ident)[0].ravel()
+    # the candidates before subsampling: with the identity "permutation" the reference keeps
+    # the first k; recompute the candidate sets from the pre-sampling rules instead
+    cfg = dict(orpn.DEFAULT_RPN)
+    cfg["batch"] = 10 ** 9  # no subsampling: every candidate keeps its label
+    cand = orpn.anchor_target(H, W, gts, im_info, BASE, 16, ident, cfg)[0].ravel()
+    fg_c, bg_c = np.nonzero(cand == 1)[0], np.nonzero(cand == 0)[0]
+    assert len(fg_c) > 128 and len(bg_c) > 256, (len(fg_c), len(bg_c))
+    t = lambda x: torch.from_numpy(x).to(dev)
+    seeds = 1200
+    cnt = torch.zeros(full.size, dtype=torch.float64, device=dev)
+    for s in range(seeds):
+        lab = anchor_target(t(BASE), H, W, 16, t(gts), t(im_info), rpn_cfg_struct(), seed=s)[0]
+        cnt += (lab.reshape(-1) >= 0).double()
+    cnt = cnt.cpu().numpy()
+    for cands, k in ((fg_c, 128), (bg_c, 256 - 128)):
+        p = k / len(cands)
+        mu, sd = seeds * p, np.sqrt(seeds * p * (1 - p))
+        z = np.abs(cnt[cands] - mu) / sd
+        assert z.max() < 5.0, (len(cands), k, float(z.max()))
+        outside = np.setdiff1d(np.arange(full.size), np.concatenate([fg_c, bg_c]))
+    assert cnt[outside].max() == 0

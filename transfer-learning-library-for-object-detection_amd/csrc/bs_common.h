@@ -19,33 +19,85 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ unsigned pack_hi2(unsigned lo_elem, unsigned hi_elem) {
-  return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);  // upper halves -> 2 x bf16
+// Exact split x = hi + mid + lo into bf16 terms, each the round-to-nearest-even bf16 of
+// the remainder (v_cvt_pk_bf16_f32, two elements per instruction; element 0 in the low
+// half).  hi keeps 8 significant bits, the remainder x - hi is exact with <= 16 bits,
+// mid its RNE 8 bits and lo the exact rest (<= 8 bits).  Round-to-nearest matters for
+// accuracy, not exactness: the products the bf16x6 scheme drops (mid*lo, lo*mid, lo*lo)
+// then have random signs — a truncating split makes every remainder carry the sign of its
+// operand, so every dropped term has the sign of its product and the sums shrink
+// systematically (~3e-8 relative per product, a coherent bias that weight gradients
+// accumulate instead of averaging out).
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+// one pair of floats -> its NPL packed bf16 planes
+template <int NPL>
+__device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m,
+                                       unsigned& l) {
+  h = cvt_pk_bf16(x0, x1);
+  const float r0 = x0 - bf_lo(h), r1 = x1 - bf_hi(h);
+  m = cvt_pk_bf16(r0, r1);
+  if constexpr (NPL == 3) l = cvt_pk_bf16(r0 - bf_lo(m), r1 - bf_hi(m));
 }
 
 // split 8 floats into NPL bf16 planes (16 B each)
 template <int NPL>
 __device__ __forceinline__ void split8(const float (&v)[8], u32x4 (&out)[3]) {
-  unsigned hb[8], mb[8], lb[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const unsigned u = __float_as_uint(v[e]);
-    hb[e] = u & 0xffff0000u;
-    const float r = v[e] - __uint_as_float(hb[e]);
-    mb[e] = __float_as_uint(r) & 0xffff0000u;
-    if constexpr (NPL == 3) lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
-  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    out[0][q] = pack_hi2(hb[2 * q], hb[2 * q + 1]);
-    out[1][q] = pack_hi2(mb[2 * q], mb[2 * q + 1]);
-    if constexpr (NPL == 3) out[2][q] = pack_hi2(lb[2 * q], lb[2 * q + 1]);
+    unsigned h, m, l = 0;
+    split2<NPL>(v[2 * q], v[2 * q + 1], h, m, l);
+    out[0][q] = h;
+    out[1][q] = m;
+    if constexpr (NPL == 3) out[2][q] = l;
   }
 }
 
 __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// One k-step of the split-bf16 product of a 32x32 tile (NP = 3 or 6 bf16 products),
+// chained into the running accumulator.  Accuracy note: the bf16 MFMA's
+// accumulation of these chains carries a small coherent shrink — measured -3e-9 relative
+// per conv layer on random data, ~-6e-8 per layer through VGG16 (none for the f32 MFMA
+// or the vendor libraries).  TLOD_BS_KSUM=1 sums each k-step's products from zero and adds
+// the sum with a VALU add (IEEE), but needs a 16-register temporary per live tile: the
+// current tilings spill with it, so it is off.
+#ifndef TLOD_BS_KSUM
+#define TLOD_BS_KSUM 0
+#endif
+template <int NP>
+__device__ __forceinline__ void bs_mac(f32x16& acc, u32x4 a0, u32x4 a1, u32x4 a2, u32x4 b0,
+                                       u32x4 b1, u32x4 b2) {
+  if (TLOD_BS_KSUM) {
+    f32x16 t = mfma_bf16(a0, b0, f32x16{});
+    t = mfma_bf16(a1, b0, t);
+    t = mfma_bf16(a0, b1, t);
+    if constexpr (NP == 6) {
+      t = mfma_bf16(a2, b0, t);
+      t = mfma_bf16(a1, b1, t);
+      t = mfma_bf16(a0, b2, t);
+    }
+    acc += t;
+  } else {
+    acc = mfma_bf16(a0, b0, acc);
+    acc = mfma_bf16(a1, b0, acc);
+    acc = mfma_bf16(a0, b1, acc);
+    if constexpr (NP == 6) {
+      acc = mfma_bf16(a2, b0, acc);
+      acc = mfma_bf16(a1, b1, acc);
+      acc = mfma_bf16(a0, b2, acc);
+    }
+  }
 }
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -72,20 +124,13 @@ __device__ __forceinline__ unsigned lt_mask4(int x) { return (1u << min(max(x, 0
 // split 4 floats into NPL bf16 planes (8 B each)
 template <int NPL>
 __device__ __forceinline__ void split4(const float (&v)[4], unsigned (&out)[3][2]) {
-  unsigned hb[4], mb[4], lb[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const unsigned u = __float_as_uint(v[e]);
-    hb[e] = u & 0xffff0000u;
-    const float r = v[e] - __uint_as_float(hb[e]);
-    mb[e] = __float_as_uint(r) & 0xffff0000u;
-    if constexpr (NPL == 3) lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));
-  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    out[0][q] = pack_hi2(hb[2 * q], hb[2 * q + 1]);
-    out[1][q] = pack_hi2(mb[2 * q], mb[2 * q + 1]);
-    if constexpr (NPL == 3) out[2][q] = pack_hi2(lb[2 * q], lb[2 * q + 1]);
+    unsigned h, m, l = 0;
+    split2<NPL>(v[2 * q], v[2 * q + 1], h, m, l);
+    out[0][q] = h;
+    out[1][q] = m;
+    if constexpr (NPL == 3) out[2][q] = l;
   }
 }
 

@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
 
 // ======================================================================= split-bf16 forward
 // The same implicit GEMM on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32-input
-// rate) with every f32 operand split exactly into three bf16 terms by truncation,
+// rate) with every f32 operand split exactly into three bf16 terms (round-to-nearest),
 // x = hi + mid + lo (hi keeps the top 8 mantissa bits, mid the next 8, lo the last 8; the
 // remainders are exact in f32).  NP = 6 accumulates lo*hi, mid*mid, hi*lo, mid*hi, hi*mid,
 // hi*hi (the dropped terms are < 2^-24 relative: f32-level error; measured normwise error
@@ -559,16 +559,8 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if constexpr (NP == 6) {
-          acc[i][j] = mfma_bf16(a[i][2], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[i][1], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[i][0], b[j][2], acc[i][j]);
-        }
-        acc[i][j] = mfma_bf16(a[i][1], b[j][0], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[i][0], b[j][1], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[i][0], b[j][0], acc[i][j]);
-      }
+      for (int j = 0; j < NJ; ++j)
+        bs_mac<NP>(acc[i][j], a[i][0], a[i][1], a[i][2], b[j][0], b[j][1], b[j][2]);
   };
 
   // Tap pairing over chunk pairs (no zero-pad MFMA work): the 18 (chunk, tap) units of the
@@ -691,7 +683,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 }
 
 // Packed, pre-split weights for conv_fwd_bs_kernel: three bf16 planes (hi, mid, lo of the
-// exact truncation split), each P[pl][o][c*80 + s*8 + e] = weight of output row o, input
+// exact round-to-nearest split), each P[pl][o][c*80 + s*8 + e] = weight of output row o, input
 // channel c*8+e, tap s (0 for s = 9 — the pad tap — and past the last channel).  dgrad = 1
 // packs the transposed, flipped operand (rows = input channels, inputs = output channels,
 // tap 8-s).
@@ -1124,14 +1116,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
         a[pl] = *reinterpret_cast<const u32x4*>(buf + a_rd + pl * C::A_PLANE + i * 32 * C::PITCH);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        if constexpr (NP == 6) {
-          acc[i][j] = mfma_bf16(a[2], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[1], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[0], b[j][2], acc[i][j]);
-        }
-        acc[i][j] = mfma_bf16(a[1], b[j][0], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0], b[j][1], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0], b[j][0], acc[i][j]);
+        bs_mac<NP>(acc[i][j], a[0], a[1], a[2], b[j][0], b[j][1], b[j][2]);
       }
     }
     if (!TLOD_MID_STORE && more) store_chunk(smem + ((it + 1) & 1) * C::BUF);

@@ -179,14 +179,7 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, f32x16 (&acc)[MI][kNJ],
         a[pl] = read_operand<AK>(buf + pl * A_PL, wm * MI * 32 + i * 32, lane);
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
-        if constexpr (NP == 6) {
-          acc[i][j] = mfma_bf16(a[2], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[1], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[0], b[j][2], acc[i][j]);
-        }
-        acc[i][j] = mfma_bf16(a[1], b[j][0], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0], b[j][1], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0], b[j][0], acc[i][j]);
+        bs_mac<NP>(acc[i][j], a[0], a[1], a[2], b[j][0], b[j][1], b[j][2]);
       }
     }
     if (!TLOD_MID_STORE && more) store(smem + ((it + 1) & 1) * BUF);

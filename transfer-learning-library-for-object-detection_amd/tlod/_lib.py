@@ -114,6 +114,8 @@ SIGNATURES = {
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_image_blob_u8": (c_int, [P, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_int, P, P]),
+    "tlod_detect_f32": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_float, c_float, c_float,
+                                c_float, c_float, P, P, P, P]),
     "tlod_space_to_depth_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_depth_to_space_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_relu_dropout_f32": (c_int, [P, P, ctypes.c_longlong, c_float, c_uint64, P]),

@@ -272,8 +272,10 @@ def relu_bwd_bias(dy, y=None, want_db=True, db_out=None):
 
 class ConvFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, relu):
+    def forward(ctx, x, weight, bias, relu, tap=None):
         y = conv_fwd(x, weight, bias, relu)
+        if tap is not None:  # test instrumentation (Conv2d.act_tap): the activation
+            tap.append(y.detach().clone())
         ctx.relu = bool(relu)
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)  # gradient slots (tlod.grads)
@@ -289,7 +291,7 @@ class ConvFunction(torch.autograd.Function):
                               db_out=grad_out(ctx.params[1]) if need_b else None)
         dx = conv_dgrad(g, weight) if need_x else None
         dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0])) if need_w else None
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def relu_bwd_ex(dy, y=None, scale=None, want_raw=False):
@@ -383,8 +385,10 @@ class ConvPoolFunction(torch.autograd.Function):
     (tlod_maxpool2x2_relu_bwd_f32) — no index tensor, no full-size pool gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, tap=None):
         y = conv_fwd(x, weight, bias, True)
+        if tap is not None:  # test instrumentation: the pre-pool activation
+            tap.append(y.detach().clone())
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
         ctx.save_for_backward(x, weight, y)
@@ -399,7 +403,7 @@ class ConvPoolFunction(torch.autograd.Function):
                                  db_out=grad_out(ctx.params[1]) if need_b else None)
         dx = conv_dgrad(g, weight) if need_x else None
         dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0])) if need_w else None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class Conv2d(nn.Conv2d):
@@ -415,6 +419,7 @@ class Conv2d(nn.Conv2d):
             raise NotImplementedError("tlod.Conv2d: stride 1, 'same' padding, 1x1/3x3 only")
         self.relu = relu
         self.pool = False  # set by the VGG16 builder: max_pool2d(2, 2) of the ReLU output
+        self.act_tap = None  # tests: a list receiving each forward's (pre-pool) activation
 
     def forward(self, x):
         if self.pool:
@@ -424,14 +429,14 @@ class Conv2d(nn.Conv2d):
                 or (self.bias is not None and self.bias.requires_grad))
             if not needs_grad:
                 return conv_fwd_pool(x, self.weight, self.bias)
-            return ConvPoolFunction.apply(x, self.weight, self.bias)
+            return ConvPoolFunction.apply(x, self.weight, self.bias, self.act_tap)
         if self.out_channels % 4:
             # GEMM-library path for the tiny 1x1 heads (e.g. 512->2 of _ImageDA.Conv2)
             assert self.kernel_size[0] == 1
             y = F.linear(x.permute(0, 2, 3, 1), self.weight.view(self.out_channels, -1), self.bias)
             y = y.permute(0, 3, 1, 2).contiguous()
             return F.relu(y) if self.relu else y
-        return ConvFunction.apply(x, self.weight, self.bias, self.relu)
+        return ConvFunction.apply(x, self.weight, self.bias, self.relu, self.act_tap)
 
     def extra_repr(self):
         return super().extra_repr() + (", relu=True" if self.relu else "") + \

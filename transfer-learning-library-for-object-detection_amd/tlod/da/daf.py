@@ -102,8 +102,8 @@ class _InstanceDA(nn.Module):
     def score(self, x):
         """The sigmoid outputs alone (the DAF forward discards the label tensor)."""
         x = grad_reverse(x)
-        x = relu_dropout(self.dc_ip1(x), self.dc_drop1)
-        x = relu_dropout(self.dc_ip2(x), self.dc_drop2)
+        x = relu_dropout(self.dc_ip1(x), self.dc_drop1, getattr(self.dc_ip1, "act_tap", None))
+        x = relu_dropout(self.dc_ip2(x), self.dc_drop2, getattr(self.dc_ip2, "act_tap", None))
         return torch.sigmoid(self.clssifer(x))
 
     def forward(self, x, need_backprop):

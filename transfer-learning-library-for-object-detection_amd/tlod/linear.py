@@ -118,7 +118,7 @@ class ReluDropoutFunction(torch.autograd.Function):
         return g, None, None
 
 
-def relu_dropout(y, dropout):
+def relu_dropout(y, dropout, tap=None):
     """dropout(relu(y)) with the nn.Dropout module's p and training mode (its RNG stream is
     libtlod's counter-based one, seeded from torch's CPU generator: no device sync; no draw
     at all when p == 0 or in eval mode, so the CPU generator's stream is left alone)."""
@@ -126,7 +126,10 @@ def relu_dropout(y, dropout):
     if not fused_act():
         return dropout(torch.relu(y))
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0.0 else 0
-    return ReluDropoutFunction.apply(y, p, seed)
+    out = ReluDropoutFunction.apply(y, p, seed)
+    if tap is not None:  # test instrumentation (Linear.act_tap): the activation
+        tap.append(out.detach().clone())
+    return out
 
 
 class FcTop(nn.Sequential):
@@ -141,7 +144,7 @@ class FcTop(nn.Sequential):
             m = mods[i]
             if (i + 2 < len(mods) and isinstance(m, nn.Linear) and isinstance(mods[i + 1], nn.ReLU)
                     and isinstance(mods[i + 2], nn.Dropout)):
-                x = relu_dropout(m(x), mods[i + 2])
+                x = relu_dropout(m(x), mods[i + 2], getattr(m, "act_tap", None))
                 i += 3
             else:
                 x = m(x)
