@@ -249,7 +249,7 @@ class OracleDAF(nn.Module):
         # target image: RPN in eval mode (TEST proposals)
         t_c3, t_c4, t_base = self._backbone(t_im)
         _, _, t_prob, t_bbox = self._rpn(t_base)
-        t_rois = orpn.proposal_layer(t__np(prob.float()), t__np(bbox.float()),
+        t_rois = orpn.proposal_layer(_np(t_prob.float()), _np(t_bbox.float()),
                                      _np(t_info.float()), self.base_anchors, c["stride"], c["pre_test"],
                                      c["post_test"], c["nms"])
         t_props = t_rois

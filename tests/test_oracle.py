@@ -98,3 +98,27 @@ def test_drm_chunks_is_cropped_pixel_unshuffle():
         Ho, Wo = 11 // s, 14 // s
         ref = F.pixel_unshuffle(x[:, :, :Ho * s, :Wo * s], s)
         assert torch.equal(drm_chunks(x, s), ref)
+
+
+def test_oracle_steps_run_on_cpu():
+    """The step oracles (test infrastructure) run end to end on a tiny batch, including the
+    fp64 run and the activation-pattern record / force machinery the GPU tests use."""
+    import copy
+
+    import torch
+
+    from helpers import record_pattern, run_in_pattern
+    from oracle.daf_step import OracleDAF, synthetic_batch, total_loss
+    torch.manual_seed(0)
+    o = OracleDAF(dropout=0.0).train()
+    b = synthetic_batch(96, 128, seed=3)
+    own = record_pattern(o, lambda: total_loss(o(b, np.random.RandomState(3))).backward())
+    assert "base.11" in own and "ip1" in own and len(own["base.11"]) == 2
+    o64 = copy.deepcopy(o).double()
+    b64 = tuple(t.double() if t.is_floating_point() else t for t in b)
+    run_in_pattern(o64, own, lambda: total_loss(o64(b64, np.random.RandomState(3))).backward())
+    g32 = dict(o.named_parameters())
+    for k, p in o64.named_parameters():
+        if p.grad is not None:
+            e = float((g32[k].grad.double() - p.grad).norm() / max(float(p.grad.norm()), 1e-30))
+            assert e < 1e-4, (k, e)
