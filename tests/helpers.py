@@ -160,7 +160,7 @@ def record_pattern(o32, fn):
         o32.forced.clear()
 
 
-def pattern_grad_bar(m, o, run, cpu_batch, taps, n_rows, own32, factor=2.0, floor=1e-5):
+def pattern_grad_bar(m, o, run, cpu_batch, taps, n_rows, own32, factor=2.0, floor=2e-5):
     """The gradient bar of the step tests, in matched activation patterns.
 
     Three fp32 gradient sets are each compared with an fp64 run of the same step (same
@@ -170,11 +170,11 @@ def pattern_grad_bar(m, o, run, cpu_batch, taps, n_rows, own32, factor=2.0, floo
       gpu32   — the same oracle with its conv / linear on this GPU in fp32 (MIOpen /
                 hipBLASLt: the arithmetic the reference's PyTorch-CUDA path uses here).
     Bar: every parameter's device error <= max(factor x max(cpu32, gpu32), floor), floor =
-    1e-5 normwise (100x inside north_star's 1e-3).  The floor is what the device needs: its
-    split-bf16 MFMA accumulation carries a small coherent shrink (-3e-9 relative per conv
-    layer on random data, ~-6e-8 per layer through VGG16) that weight
-    gradients sum up to 1e-6..6e-6, where the fp32 references stay at 2e-7..1.5e-6 — the
-    printed ratios keep that gap visible.  ``run(model, batch)`` returns the oracle's total
+    2e-5 normwise (50x inside north_star's 1e-3).  The floor is what the device needs: its
+    split-bf16 MFMA path carries a small coherent shrink (~-6e-8 relative per conv layer
+    through VGG16, none with the f32 MFMA) that the input-gradient chain
+    compounds: conv3_1's gradients end at 1e-5 at most, where the fp32 references stay at
+    2e-7..1.5e-6 — the printed ratios keep that gap visible.  ``run(model, batch)`` returns the oracle's total
     loss; ``own32`` is the cpu32 run's recorded pattern (the caller already ran it)."""
     import copy
     import torch

@@ -183,87 +183,53 @@ __global__ void __launch_bounds__(kAvgThreads) roi_align_avg_bwd_kernel(
 }
 
 // ------------------------------------------------------------ RoIAlignAvg backward, NHWC
-// One workgroup per (roi, 64 channels), lane = channel.  The RoI's (ph+1)x(pw+1) samples
-// touch the cells {gy, gy+1} x {gx, gx+1}: at most 16 distinct rows x 16 distinct columns,
-// far fewer when the RoI spans fewer cells than it has samples (a 3x3-cell RoI: 5x5 cells
-// for 256 taps).  The four waves split the samples and add each tap into a per-RoI LDS
-// footprint (ds_add_f32, conflict-free: lane = channel = LDS bank); the footprint is then
-// flushed with one global atomic per (cell, channel) — 64 consecutive channels of one cell
-// per wave instruction, 256 contiguous bytes of the (B,H,W,C) accumulator, the shape the
-// memory-side atomic unit runs at full rate.  Tap values are the reference's atomicAdd
-// arguments (roi_align_kernel.cu:137-140); as there, the accumulation order is not fixed.
-constexpr int kNhwcCh = 64;
+// One thread per channel, one workgroup per (roi, 256 channels): every atomic
+// wave-instruction adds 64 consecutive channels of one feature cell = 256 contiguous
+// bytes of the (B,H,W,C) accumulator — the shape the memory-side atomic unit runs at
+// full rate (one lane per row, the NCHW shape, runs ~17x slower).
 constexpr int kNhwcThreads = 256;
-constexpr int kMaxAxis = 16;  // distinct tap rows / columns of one RoI (8 samples x 2)
 
 __global__ void __launch_bounds__(kNhwcThreads) roi_align_avg_bwd_nhwc_kernel(
     const float* __restrict__ top, float scale, int C, int H, int W, int ph, int pw,
     const float* __restrict__ rois, float* __restrict__ acc_nhwc) {
   const int ah = ph + 1, aw = pw + 1, P = ph * pw;
-  const int r = blockIdx.y, c0 = blockIdx.x * kNhwcCh;
-  const int nc = min(kNhwcCh, C - c0);
+  const int r = blockIdx.y, c0 = blockIdx.x * kNhwcThreads;
+  const int nc = min(kNhwcThreads, C - c0);
   __shared__ int gy[8], gx[8];
   __shared__ float ghr[8], gwr[8];
   __shared__ bool gvy[8], gvx[8];
-  __shared__ int rows[kMaxAxis], cols[kMaxAxis], ry[8], cx[8], n_rows, n_cols;
-  __shared__ float g7[kNhwcCh * 49];
-  __shared__ float foot[kMaxAxis * kMaxAxis * kNhwcCh];
+  __shared__ float g7[kNhwcThreads * 49];
   const float* ro = rois + r * 5;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   if (t < ah) align_axis(ro[2] * scale, ro[4] * scale, ah, t, H, &gy[t], &ghr[t], &gvy[t]);
-  if (t >= 64 && t < 64 + aw) {
-    const int p = t - 64;
+  if (t >= 32 && t < 32 + aw) {
+    const int p = t - 32;
     align_axis(ro[1] * scale, ro[3] * scale, aw, p, W, &gx[p], &gwr[p], &gvx[p]);
   }
   const float* tp = top + ((size_t)r * C + c0) * P;
   for (int e = t; e < nc * P; e += kNhwcThreads) g7[e] = tp[e] / 4.f;  // coalesced slab
   __syncthreads();
-  // distinct tap rows / columns (gy, gx are non-decreasing along the samples)
-  if (t == 0 || t == 64) {
-    const bool is_row = t == 0;
-    const int n = is_row ? ah : aw;
-    const int* g = is_row ? gy : gx;
-    const bool* v = is_row ? gvy : gvx;
-    int* list = is_row ? rows : cols;
-    int* at = is_row ? ry : cx;
-    int k = 0;
-    for (int i = 0; i < n; ++i) {
-      if (!v[i]) continue;
-      const int a = g[i];
-      if (k == 0 || list[k - 1] < a) list[k++] = a;
-      at[i] = list[k - 1] == a ? k - 1 : k - 2;  // the last entry is a or a + 1
-      if (list[k - 1] < a + 1) list[k++] = a + 1;  // so list[at[i] + 1] == a + 1
-    }
-    if (is_row) n_rows = k; else n_cols = k;
-  }
-  __syncthreads();
-  const int NR = n_rows, NC = n_cols, cells = NR * NC;
-  for (int e = t; e < cells * kNhwcCh; e += kNhwcThreads) foot[e] = 0.f;
-  __syncthreads();
-  if (lane < nc) {
-    const float* gp = g7 + lane * P;
-    for (int s = wave; s < ah * aw; s += kNhwcThreads / 64) {
-      const int sy = s / aw, sx = s % aw;
-      if (!(gvy[sy] && gvx[sx])) continue;
+  if (t >= nc) return;
+  const int b = (int)ro[0];
+  float* base = acc_nhwc + (size_t)b * H * W * C + c0 + t;
+  const float* gp = g7 + t * P;
+  for (int sy = 0; sy < ah; ++sy) {
+    if (!gvy[sy]) continue;
+    const int y = gy[sy];
+    const float hr = ghr[sy];
+    for (int sx = 0; sx < aw; ++sx) {
+      if (!gvx[sx]) continue;
       float g = 0.f;  // avg_pool2d backward: py outer, px inner
       for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
         for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
-      const float hr = ghr[sy], wr = gwr[sx], om = 1.f - wr;
-      // rows[ry] = gy, rows[ry + 1] = gy + 1 (both were inserted in order); same for cols
-      float* f = foot + (ry[sy] * NC + cx[sx]) * kNhwcCh + lane;
-      atomicAdd(f, (float)(((double)g * (1. - (double)hr)) * (double)om));
-      atomicAdd(f + kNhwcCh, (float)(((double)g * (1. - (double)hr)) * (double)wr));
-      atomicAdd(f + NC * kNhwcCh, (g * hr) * om);
-      atomicAdd(f + NC * kNhwcCh + kNhwcCh, (g * hr) * wr);
+      const int x = gx[sx];
+      const float wr = gwr[sx], om = 1.f - wr;
+      float* p00 = base + ((size_t)y * W + x) * C;
+      atomicAdd(p00, (float)(((double)g * (1. - (double)hr)) * (double)om));
+      atomicAdd(p00 + C, (float)(((double)g * (1. - (double)hr)) * (double)wr));
+      atomicAdd(p00 + (size_t)W * C, (g * hr) * om);
+      atomicAdd(p00 + (size_t)W * C + C, (g * hr) * wr);
     }
-  }
-  __syncthreads();
-  if (lane >= nc) return;
-  const int b = (int)ro[0];
-  float* base = acc_nhwc + (size_t)b * H * W * C + c0 + lane;
-  for (int cell = wave; cell < cells; cell += kNhwcThreads / 64) {
-    const float v = foot[cell * kNhwcCh + lane];
-    if (v != 0.f) atomicAdd(base + ((size_t)rows[cell / NC] * W + cols[cell % NC]) * C, v);
   }
 }
 
@@ -401,7 +367,7 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
   }
   float* acc = static_cast<float*>(ws);
   TLOD_HIP(hipMemsetAsync(acc, 0, (size_t)B * C * H * W * sizeof(float), s));
-  hipLaunchKernelGGL(roi_align_avg_bwd_nhwc_kernel, dim3(div_up(C, kNhwcCh), R),
+  hipLaunchKernelGGL(roi_align_avg_bwd_nhwc_kernel, dim3(div_up(C, kNhwcThreads), R),
                      dim3(kNhwcThreads), 0, s, top_grad, scale, C, H, W, ph, pw, rois, acc);
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
