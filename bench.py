@@ -41,13 +41,23 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--width", type=int, default=1200)
-    ap.add_argument("--cpu-baseline-steps", type=int, default=2,
-                    help="oracle CPU steps timed on rank 0 at N=1 (0 disables)")
+    ap.add_argument("--cpu-baseline-steps", type=int, default=5,
+                    help="oracle CPU steps timed on rank 0 at N=1, after 2 untimed (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="torch CPU threads of the baseline (the box's share of one GPU is 16)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--net", choices=("vgg16", "res101"), default="vgg16")
     ap.add_argument("--method", choices=("daf", "maf", "atf"), default="daf",
                     help="detector (the headline metric is DAF; MAF / ATF are secondary workloads)")
     return ap.parse_args()
+
+
+def conv_bytes(kind, shape):
+    """Algorithmic HBM bytes of one conv launch: each operand read once, the result written
+    once (fp32).  shape = (N, Cin, H, W, Cout, KS) of the forward convolution."""
+    N, Cin, H, W, Cout, KS = shape
+    x, y, w = N * Cin * H * W * 4, N * Cout * H * W * 4, Cout * Cin * KS * KS * 4
+    return x + y + w  # fwd: X, W -> Y; dgrad: dY, W -> dX; wgrad: dY, X -> dW
 
 
 def conv_roofline(records):
@@ -58,10 +68,11 @@ def conv_roofline(records):
         tot_f += flops
         tot_ms += ms
         for key, table in ((kind, by), ((kind,) + tuple(shape), shapes)):
-            d = table.setdefault(key, [0.0, 0.0, 0])
+            d = table.setdefault(key, [0.0, 0.0, 0, 0.0])
             d[0] += flops
             d[1] += ms
             d[2] += 1
+            d[3] += conv_bytes(kind, shape)
     if os.environ.get("TLOD_BENCH_SHAPES"):
         for k, v in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
             print(f"{k[0]:6s} N={k[1]} Cin={k[2]:4d} {k[3]:4d}x{k[4]:<4d} Cout={k[5]:4d} KS={k[6]} "
@@ -76,42 +87,55 @@ def conv_roofline(records):
     # the dominant kernel family (most time): its own achieved / peak
     fam = {}
     for k, v in by.items():
-        f = fam.setdefault(k.split("/")[1], [0.0, 0.0])
-        f[0] += v[0]
-        f[1] += v[1]
+        f = fam.setdefault(k.split("/")[1], [0.0, 0.0, 0, 0.0])
+        for i in range(4):
+            f[i] += v[i]
     dom = max(fam, key=lambda m: fam[m][1])
     dominant = {"math": dom, "achieved": fam[dom][0] / (fam[dom][1] * 1e-3) / 1e12,
-                "peak": PEAKS[dom], "ms": fam[dom][1]}
+                "peak": PEAKS[dom], "ms": fam[dom][1], "launches": fam[dom][2],
+                "bytes": fam[dom][3]}
     return achieved, detail, tot_ms, tot_f, len(records), dominant
 
 
 def measured_traffic(a):
-    """HBM bytes per conv call from the latest committed PMC passes (profiles/r*/
-    conv_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE over the conv
-    kernels of this same bench command); None for workloads it was not measured on."""
+    """Per-kernel HBM bytes per step from the latest committed PMC passes of this same bench
+    command (profiles/r*/traffic.json, tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE per
+    kernel); None for workloads it was not measured on."""
     import glob
     if (a.method, a.net, a.height, a.width) != ("daf", "vgg16", 600, 1200):
         return None, None
     here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", "r*", "conv_traffic.json")))
+    files = sorted(glob.glob(os.path.join(here, "profiles", "r*", "traffic.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        t = json.load(f)
-    return t["bytes_per_call"], os.path.relpath(files[-1], here)
+        return json.load(f), os.path.relpath(files[-1], here)
 
 
-def cpu_baseline(steps, H, W):
-    """The oracle's CPU DAF step (test-infrastructure restatement) on this host's cores."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(steps, H, W, threads):
+    """The oracle's CPU DAF step (test-infrastructure restatement) on this host's cores:
+    2 untimed + ``steps`` timed steps, the median."""
     import oracle.daf_step as ods
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(threads, 64))
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(threads, avail))
     torch.set_num_threads(threads)
-    t = ods.time_cpu_steps(steps, H, W)
+    t = ods.time_cpu_steps(steps, H, W, warmup=2)
     return {"value": round(1.0 / t, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} DAF-VGG16 steps (1 src + 1 tgt image {H}x{W}, synthetic) of the "
-                      f"oracle restatement: numpy RPN/NMS/RoIAlign + torch-CPU fp32 conv/linear; "
-                      f"mean s/step = {t:.2f}"}
+            "cpu_model": cpu_model(),
+            "sample": f"2 untimed + {steps} timed DAF-VGG16 steps (1 src + 1 tgt image {H}x{W}, "
+                      f"synthetic) of the oracle restatement: numpy RPN/NMS/RoIAlign + torch-CPU "
+                      f"fp32 conv/linear, {threads} threads; median s/step = {t:.2f}"}
 
 
 def main():
@@ -122,8 +146,12 @@ def main():
     from tlod.detector.train import (SyntheticCityscapes, build_model, make_optimizer,
                                      train_step)
 
-    rank, world = init_from_env()
+    # TLOD_DIST_BACKEND=gloo: the multi-rank path on one GPU (ranks share cuda:0) — a
+    # plumbing rehearsal of the RCCL run, not a measurement
+    rank, world = init_from_env(os.environ.get("TLOD_DIST_BACKEND"))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if os.environ.get("TLOD_DIST_BACKEND") == "gloo":
+        local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     model = build_model(a.method, dev, a.net)
@@ -164,7 +192,13 @@ def main():
     last_loss = float(torch.stack(losses).float().mean().item())
 
     achieved, detail, conv_ms, conv_f, n_launch, dom = conv_roofline(records)
-    traffic_bytes, traffic_src = measured_traffic(a)
+    traffic, traffic_src = measured_traffic(a)
+    dom_kernels = ("conv_fwd_bs_kernel", "conv_wgrad_bs_kernel") if dom["math"] != "f32" else \
+        ("conv_fwd_kernel", "conv_wgrad_kernel")
+    per_launch_pmc = None
+    if traffic:
+        per_launch_pmc = round(sum(traffic["bytes_per_step_by_kernel"].get(k, 0)
+                                   for k in dom_kernels) / (dom["launches"] / a.steps))
     result = {
         "metric": METRIC.replace("DAF VGG16", f"{a.method.upper()} {'VGG16' if a.net == 'vgg16' else 'ResNet101'}"),
         "value": round(value, 4), "unit": "img/s", "n_gpus": world,
@@ -182,9 +216,17 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(dom["achieved"], 2),
                      "peak": round(dom["peak"], 1), "unit": "TFLOP/s",
                      "frac": round(dom["achieved"] / dom["peak"], 4),
-                     "traffic": traffic_bytes, "traffic_source": traffic_src,
+                     "traffic": per_launch_pmc,
+                     "algorithmic_bytes": round(dom["bytes"] / dom["launches"]),
+                     "traffic_source": traffic_src,
+                     "traffic_note": "PMC HBM bytes per launch of the dominant kernels "
+                                     f"({' + '.join(dom_kernels)}; FETCH_SIZE x2 + WRITE_SIZE) "
+                                     "vs algorithmic bytes per launch (operands read once, "
+                                     "result written once)",
+                     "traffic_by_kernel_per_step": (traffic or {}).get("bytes_per_step_by_kernel"),
                      "kernel": f"tlod 3x3/1x1 conv, {dom['math']} arithmetic "
                                "(the family with the most time in the step)",
+                     "kernel_ms_per_step": round(dom["ms"] / a.steps, 3),
                      "peak_basis": "f32-equivalent: algorithmic f32 FLOPs at the MFMA peak; "
                                    "bf16xN = 2516.6 TF bf16 dense / N products",
                      "all_conv": {"achieved": round(achieved, 2), "launches": n_launch,
@@ -198,7 +240,8 @@ def main():
     }
     if rank == 0 and world == 1 and a.cpu_baseline_steps > 0 and a.method == "daf" \
             and a.net == "vgg16":
-        result["cpu_baseline"] = cpu_baseline(a.cpu_baseline_steps, a.height, a.width)
+        result["cpu_baseline"] = cpu_baseline(a.cpu_baseline_steps, a.height, a.width,
+                                              a.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

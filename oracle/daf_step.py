@@ -313,8 +313,9 @@ def synthetic_batch(H, W, seed=1, G=8):
             img(), info.clone(), torch.ones(1, 5), torch.zeros(1, dtype=torch.long), torch.zeros(1))
 
 
-def time_cpu_steps(steps, H=600, W=1200):
-    """Mean seconds per full DAF step (fwd + bwd + clip + SGD) on the CPU."""
+def time_cpu_steps(steps, H=600, W=1200, warmup=0):
+    """Seconds per full DAF step (fwd + bwd + clip + SGD) on the CPU: the median of
+    ``steps`` timed steps after ``warmup`` untimed ones (2 + 5)."""
     torch.manual_seed(0)
     m = OracleDAF().train()
     params = [p for p in m.parameters() if p.requires_grad]
@@ -322,7 +323,7 @@ def time_cpu_steps(steps, H=600, W=1200):
     batch = synthetic_batch(H, W)
     rng = np.random.RandomState(3)
     times = []
-    for _ in range(steps):
+    for i in range(warmup + steps):
         t0 = time.perf_counter()
         opt.zero_grad()
         loss = total_loss(m(batch, rng))
@@ -333,5 +334,6 @@ def time_cpu_steps(steps, H=600, W=1200):
             if p.grad is not None:
                 p.grad.mul_(scale)
         opt.step()
-        times.append(time.perf_counter() - t0)
-    return float(np.mean(times))
+        if i >= warmup:
+            times.append(time.perf_counter() - t0)
+    return float(np.median(times))
