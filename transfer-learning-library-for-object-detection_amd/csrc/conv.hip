@@ -50,6 +50,9 @@ namespace tlod {
 #ifndef TLOD_TAP_PAIRING
 #define TLOD_TAP_PAIRING 1
 #endif
+#ifndef TLOD_WS_PRIO
+#define TLOD_WS_PRIO 0
+#endif
 #ifndef TLOD_CONV_OCC
 #define TLOD_CONV_OCC __attribute__((amdgpu_waves_per_eu(2, 4)))
 #endif
@@ -680,6 +683,529 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
         }
       }
     }
+}
+
+// ------------------------------------------------------------ warp-specialized variant
+// conv_fwd_bs_kernel's tile (64 output channels x 16 x 32 pixels) and K order, with
+//  * the staging on kProdWaves extra producer waves (one per SIMD): the 8 MFMA waves only
+//    read LDS fragments and issue MFMAs, so the global-load waits, the split VALU and the
+//    LDS stores of the next chunk overlap the other waves' MFMAs instead of stalling both
+//    waves of a SIMD at once;
+//  * 16x16x32 MFMAs (v_mfma_f32_16x16x32_bf16): the chip holds a higher clock on this shape
+//    than on 32x32x16 for the same work (measured 2.10 vs 1.95 GHz on conv3_3);
+//  * persistent workgroups: a workgroup walks work items (whole tiles, then split-K pieces)
+//    b, b + G, ..., so the producers stage the next item's first chunks while the MFMA
+//    waves run the previous item's epilogue (one workgroup per CU: nothing else overlaps it).
+// Per chunk pair (chunk c in LDS buffer 0, c+1 in buffer 1; 18 (tap, 8-channel) units =
+// four 16x16x32 steps of 4 units + one 16x16x16 step of 2):
+//   steps 0-1   producers store chunk c+1 into buffer 1 (all but an item's first pair) and
+//               load chunk c+2
+//   barrier     (chunk c+1 visible)
+//   step 2      units 8..11: straddles the buffers
+//   barrier     (buffer 0 retired)
+//   steps 3-4   producers store chunk c+2 into buffer 0 and load chunk c+3
+//   barrier
+// Producers and MFMA waves run separate loops with the same barrier sequence, so neither
+// carries the other's registers (the kernel fits 3 waves per SIMD).
+constexpr int kProdWaves = 4;
+
+// Diagnostic build only (TLOD_WS_STAMPS=1; never in the shipped library): per-wave sums of
+// s_memtime cycles per pipeline segment of the warp-specialized loop, for blocks < 256,
+// read back with tlod_debug_ws_stamps.  Segment k = cycles from stamp k-1 to stamp k.
+#ifndef TLOD_WS_STAMPS
+#define TLOD_WS_STAMPS 0
+#endif
+// producer loads: 1 = flat global loads (invalid elements read g_zero), 0 = raw buffer
+// loads (invalid elements read past the range: 0)
+#ifndef TLOD_WS_FLAT
+#define TLOD_WS_FLAT 2
+#endif
+#ifndef TLOD_WS_ROT
+#define TLOD_WS_ROT 1
+#endif
+#if TLOD_WS_STAMPS
+__device__ unsigned long long g_ws_stamps[256 * 12 * 8];
+__device__ unsigned long long g_ws_clock[512];
+#define WS_STAMP_DECL                                \
+  unsigned long long ws_seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  const unsigned long long ws_t0 = __builtin_amdgcn_s_memtime(); \
+  const unsigned long long ws_r0 = __builtin_amdgcn_s_memrealtime(); \
+  unsigned long long ws_t = ws_t0
+#define WS_STAMP(k)                                              \
+  do {                                                           \
+    const unsigned long long now = __builtin_amdgcn_s_memtime(); \
+    if ((k) >= 0) ws_seg[(k) < 0 ? 0 : (k)] += now - ws_t;       \
+    ws_t = now;                                                  \
+  } while (0)
+#define WS_STAMP_SAVE                                                            \
+  do {                                                                           \
+    if (blockIdx.x < 256 && (threadIdx.x & 63) == 0)                             \
+      for (int k_ = 0; k_ < 8; ++k_)                                             \
+        g_ws_stamps[(blockIdx.x * 12 + threadIdx.x / 64) * 8 + k_] = ws_seg[k_]; \
+    if (blockIdx.x < 256 && threadIdx.x == 0) {                                  \
+      g_ws_clock[blockIdx.x * 2] = __builtin_amdgcn_s_memtime() - ws_t0;         \
+      g_ws_clock[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime() - ws_r0; \
+    }                                                                            \
+  } while (0)
+#else
+#define WS_STAMP_DECL do {} while (0)
+#define WS_STAMP(k) do {} while (0)
+#define WS_STAMP_SAVE do {} while (0)
+#endif
+
+// LDS image: weight rows at a 160-B pitch (10 slots: the 16-lane groups of a ds_read_b128
+// read rows r and r+4.. of two units an odd number of slots apart — conflict-free), a
+// buffer of an odd number of 16-B slots (the unit pair that straddles the two buffers stays
+// odd apart), and two (bias, scale) slots for consecutive work items.
+template <int WM, int WN, int MI, int NJ, int NP>
+struct WsCfg : BsCfg<WM, WN, MI, NJ, NP, false> {
+  using B = BsCfg<WM, WN, MI, NJ, NP, false>;
+  static constexpr int AROW = 160;
+  static constexpr int A_PLANE = B::BM * AROW;
+  static constexpr int BUF0 = B::NPL * (A_PLANE + B::B_PLANE);
+  static constexpr int BUF = (BUF0 / 16) % 2 == 0 ? BUF0 + 16 : BUF0;
+  static constexpr int LDS_BYTES = 2 * BUF + 4 * B::BM * 4;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x4 mfma16_bf16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16k16_bf16(u32x2 a, u32x2 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(bf16x4, a),
+                                                   __builtin_bit_cast(bf16x4, b), c, 0, 0, 0);
+}
+// bs_mac's product order (a0b0, a1b0, a0b1, a2b0, a1b1, a0b2) on a 16x16 tile
+template <int NP, typename V, typename F>
+__device__ __forceinline__ void bs_mac16(f32x4& acc, const V (&a)[3], const V (&b)[3], F mf) {
+  acc = mf(a[0], b[0], acc);
+  acc = mf(a[1], b[0], acc);
+  acc = mf(a[0], b[1], acc);
+  if constexpr (NP == 6) {
+    acc = mf(a[2], b[0], acc);
+    acc = mf(a[1], b[1], acc);
+    acc = mf(a[0], b[2], acc);
+  }
+}
+
+// One work item: a whole tile (direct) or one split-K piece of a tail tile, decoded from its
+// index exactly as conv_fwd_bs_kernel decodes its block id.
+struct WsItem {
+  int direct, split, ti, n, m0, h0, w0, c_begin, c_end;
+};
+__device__ __forceinline__ WsItem ws_item(int v, int tiles_m, int tiles_w, int tiles_h,
+                                          int dp_tiles, int n_tail, int ksplit, int cps,
+                                          int nchunks, int BM, int TH, int TW) {
+  WsItem it;
+  int t;
+  it.direct = v < dp_tiles;
+  if (it.direct) {
+    t = xcd_remap(v, dp_tiles);
+    it.split = it.ti = 0;
+  } else {
+    const int u = xcd_remap(v - dp_tiles, n_tail * ksplit);
+    it.ti = u % n_tail;
+    it.split = u / n_tail;
+    t = dp_tiles + it.ti;
+  }
+  const int mt = t % tiles_m; t /= tiles_m;
+  const int tw = t % tiles_w; t /= tiles_w;
+  const int th = t % tiles_h; t /= tiles_h;
+  it.n = t;
+  it.m0 = mt * BM;
+  it.w0 = tw * TW;
+  it.h0 = th * TH;
+  it.c_begin = it.direct ? 0 : it.split * cps;
+  it.c_end = it.direct ? nchunks : min(nchunks, it.c_begin + cps);
+  return it;
+}
+
+template <int WM, int WN, int MI, int NJ, int NP>
+__global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
+    __attribute__((amdgpu_waves_per_eu(3, 3))) conv_fwd_bs_ws_kernel(
+        const float* __restrict__ X, const unsigned short* __restrict__ Wp, Epi epi,
+        float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int tiles_m, int tiles_w,
+        int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab) {
+  using C = WsCfg<WM, WN, MI, NJ, NP>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int n_tiles = tiles_m * tiles_w * tiles_h * N;
+  const int n_tail = n_tiles - dp_tiles;
+  const int n_items = dp_tiles + (ksplit > 1 ? n_tail * ksplit : 0);
+  const int HWi = H * W;
+  const int nchunks = (Cin + C::CK - 1) / C::CK;
+  const int tid = threadIdx.x;
+  auto item = [&](int v) {
+    return ws_item(v, tiles_m, tiles_w, tiles_h, dp_tiles, n_tail, ksplit, cps, nchunks, C::BM,
+                   C::TH, C::TW);
+  };
+  // This workgroup's items are b, b + G, ...; odd workgroups take them in rotated order
+  // (last first), so that the workgroups' epilogue store bursts do not all coincide when the
+  // last item is a short split-K piece.
+  const int G = gridDim.x;
+  const int n_mine = (n_items - (int)blockIdx.x + G - 1) / G;
+  const int rot = TLOD_WS_ROT && (blockIdx.x & 1) ? n_mine - 1 : 0;
+  auto vidx = [&](int k) { return (int)blockIdx.x + G * ((k + rot) % n_mine); };
+
+  if (tid >= C::NT) {
+    // ================= producers: stage chunks into the two LDS buffers
+    // The producers walk the workgroup's chunk stream (item b's chunks, then item b + G's, ...)
+    // one chunk ahead in registers: every LDS store is followed by the load of the next chunk
+    // of the stream, across item boundaries.  Validity (rows past Cout, positions outside the
+    // map, channels past Cin) is applied at load time by the buffer range check (offset
+    // kBufOOB reads 0), so a chunk in registers carries no item state.  An item with an even
+    // chunk count stores the next item's first chunk into buffer 0 in its last pair's steps
+    // 3-4 (buffer 0 is retired by then), so the next item starts without a load round trip.
+    constexpr int PT = kProdWaves * 64;
+    const int ptid = tid - C::NT;
+    const unsigned wrow = (unsigned)nchunks * kBsKP;  // packed row length (bf16)
+    const unsigned wplane = (unsigned)Cout * wrow;    // packed plane length (bf16)
+    const i32x4 w_rsrc = make_buffer_rsrc(Wp, wplane * C::NPL * 2u);
+    constexpr int A_SEG = kBsKP / 8;
+    constexpr int A_N = C::NPL * C::BM * A_SEG;
+    constexpr int A_IT = (A_N + PT - 1) / PT;
+    constexpr int B_IT = (C::BPOS + PT - 1) / PT;
+    int a_lds[A_IT], a_row[A_IT];
+    unsigned a_pq[A_IT];  // plane offset + segment (elements), item-independent
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      const int idx = ptid + i * PT;
+      const int pl = idx / (C::BM * A_SEG), rem = idx % (C::BM * A_SEG);
+      const int row = rem / A_SEG, q = rem % A_SEG;
+      a_lds[i] = idx < A_N ? pl * C::A_PLANE + row * C::AROW + 16 * q : -1;
+      a_row[i] = idx < A_N ? row : 1 << 30;
+      a_pq[i] = (unsigned)pl * wplane + 8u * q;
+    }
+    int b_pos[B_IT];
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      const int pos = ptid + i * PT;
+      b_pos[i] = pos < C::PP ? C::NPL * C::A_PLANE + pos * 16 : -1;
+    }
+    WS_STAMP_DECL;
+    // load cursor: item ld (index v_ld), chunk ch_ld
+    int k_ld = 0;
+    WsItem ld = item(vidx(0));
+    int ch_ld = ld.c_begin;
+    int a_off[A_IT], b_goff[B_IT];
+    i32x4 x_rsrc;
+    auto set_ld_item = [&]() {
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i)
+        a_off[i] = ld.m0 + a_row[i] < Cout ? (int)((a_pq[i] + (unsigned)(ld.m0 + a_row[i]) * wrow) * 2u) : -1;
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i) {
+        const int pos = ptid + i * PT;
+        const int r = pos / C::PW, c = pos % C::PW;
+        const int gh = ld.h0 - 1 + r, gw = ld.w0 - 1 + c;
+        b_goff[i] = pos < C::PP && gh >= 0 && gh < H && gw >= 0 && gw < W ? gh * W + gw : -1;
+      }
+      x_rsrc = make_buffer_rsrc(X + (size_t)ld.n * Cin * HWi, (unsigned)Cin * HWi * 4u);
+    };
+    u32x4 ra[A_IT];
+    float rb[B_IT][8];
+    int ld_nv = 8;
+    unsigned ld_amask = ~0u, ld_bmask = ~0u;
+    auto load = [&]() {
+      const int ci0 = ch_ld * C::CK;
+      const int nv = min(C::CK, Cin - ci0);
+#if TLOD_WS_FLAT == 2
+      // unconditional loads (invalid: offset 0 / the last channel), masked right after
+      const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp) + ch_ld * (kBsKP * 2);
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i) ra[i] = *reinterpret_cast<const u32x4*>(Wb + max(a_off[i], 0));
+      const float* Xc = X + (size_t)ld.n * Cin * HWi + (size_t)ci0 * HWi;
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rb[i][e] = Xc[min(e, nv - 1) * HWi + max(b_goff[i], 0)];
+      ld_nv = nv;
+      ld_amask = 0;
+      ld_bmask = 0;
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i) ld_amask |= (unsigned)(a_off[i] >= 0) << i;
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i) ld_bmask |= (unsigned)(b_goff[i] >= 0) << i;
+#elif TLOD_WS_FLAT
+      const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp) + ch_ld * (kBsKP * 2);
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i)
+        ra[i] = *reinterpret_cast<const u32x4*>(a_off[i] >= 0 ? Wb + a_off[i]
+                                                              : reinterpret_cast<const unsigned char*>(g_zero));
+      const float* Xc = X + (size_t)ld.n * Cin * HWi + (size_t)ci0 * HWi;
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          rb[i][e] = *(b_goff[i] >= 0 && e < nv ? Xc + e * HWi + b_goff[i] : g_zero);
+#else
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i)
+        ra[i] = __builtin_bit_cast(
+            u32x4, raw_buffer_load_v4f32(w_rsrc, a_off[i] >= 0 ? a_off[i] + ch_ld * (kBsKP * 2) : kBufOOB, 0, 0));
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          rb[i][e] = raw_buffer_load_f32(
+              x_rsrc, b_goff[i] >= 0 && e < nv ? ((ci0 + e) * HWi + b_goff[i]) * 4 : kBufOOB, 0, 0);
+#endif
+    };
+    auto advance = [&]() {  // the next chunk of the stream; false past its end
+      if (++ch_ld < ld.c_end) return true;
+      if (++k_ld >= n_mine) return false;
+      ld = item(vidx(k_ld));
+      ch_ld = ld.c_begin;
+      set_ld_item();
+      return true;
+    };
+    auto store = [&](unsigned char* buf) {  // registers -> buf, then load the next chunk
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i)
+        if (a_lds[i] >= 0)
+          *reinterpret_cast<u32x4*>(buf + a_lds[i]) =
+              TLOD_WS_FLAT != 2 || ((ld_amask >> i) & 1) ? ra[i] : u32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i) {
+        if (b_pos[i] < 0) continue;
+        u32x4 sp[3];
+        float v8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v8[e] = TLOD_WS_FLAT != 2 || (((ld_bmask >> i) & 1) && e < ld_nv) ? rb[i][e] : 0.f;
+        split8<C::NPL>(v8, sp);
+#pragma unroll
+        for (int pl = 0; pl < C::NPL; ++pl)
+          *reinterpret_cast<u32x4*>(buf + b_pos[i] + pl * C::B_PLANE) = sp[pl];
+      }
+      WS_STAMP(6);
+      if (advance()) load();
+      WS_STAMP(7);
+    };
+    set_ld_item();
+    load();
+    bool prefetched = false;
+    for (int k = 0; k < n_mine; ++k) {
+      const WsItem it = item(vidx(k));
+      const int c_begin = it.c_begin, c_end = it.c_end;
+      const bool more = k + 1 < n_mine;
+      // the previous item's last barrier retired both buffers: its epilogue overlaps this
+      if (!prefetched) store(smem);                   // chunk c_begin
+      if (c_end - c_begin >= 2) store(smem + C::BUF);  // chunk c_begin + 1
+      __syncthreads();
+      for (int c = c_begin; c + 1 < c_end; c += 2) {
+        WS_STAMP(-1);
+        if (c != c_begin) store(smem + C::BUF);  // chunk c+1
+        WS_STAMP(0);
+        __syncthreads();
+        WS_STAMP(1);
+        __syncthreads();
+        WS_STAMP(3);
+        if (c + 2 < c_end || (c + 2 == c_end && more)) store(smem);  // chunk c+2 / next item's first
+        WS_STAMP(4);
+        __syncthreads();
+        WS_STAMP(5);
+      }
+      prefetched = ((c_end - c_begin) & 1) == 0 && more;
+      if ((c_end - c_begin) & 1) __syncthreads();  // the lone last chunk retires buffer 0
+    }
+    WS_STAMP_SAVE;
+    return;
+  }
+
+  // ================= MFMA waves
+  // The wave's 64 x 64 output block is 4 x 4 tiles of 16 x 16 (row block rb = 16 output
+  // channels; column block cb = (pixel row j, half hh) = 16 pixels).  One k-step takes four
+  // (tap, 8-channel) units, lane group g = lane / 16 reading unit 4s + g; the 16x16x16 step
+  // takes units 16, 17 (lanes 0-31 / 32-63, 8-B halves by (lane / 16) & 1).
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l16 = lane & 15, g = lane >> 4;
+  constexpr int RB = MI * 2, CB = NJ * 2;
+  const int a_lane = (wm * MI * 32 + l16) * C::AROW;
+  auto tap_c = [&](int tap) { return ((tap / 3) * C::PW + tap % 3) * 16; };
+  // column block cb sits at a compile-time offset from column block 0
+  const int bp0 = C::NPL * C::A_PLANE + (wn * NJ * C::PW + l16) * 16;
+  auto baddr = [&](int cb, int bo) { return bo + ((cb >> 1) * C::PW + (cb & 1) * 16) * 16; };
+  auto ua = [&](int u) { return (u >= 9 ? C::BUF : 0) + 16 * (u % 9); };
+  auto ub = [&](int u) { return (u >= 9 ? C::BUF : 0) + tap_c(u % 9); };
+  int aoff[4], boff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    aoff[s] = a_lane + ua(4 * s + g);
+    boff[s] = bp0 + ub(4 * s + g);
+  }
+  const int hb = 8 * (g & 1);
+  const int aoff4 = a_lane + ua(16 + (lane >> 5)) + hb;
+  const int boff4 = bp0 + ub(16 + (lane >> 5)) + hb;
+  // lone last chunk: (8, pad) — slot 9 of a weight row is zero
+  const int aoffL = a_lane + 16 * (8 + (lane >> 5)) + hb, boffL = bp0 + tap_c(8) + hb;
+
+  f32x4 acc[RB][CB];
+  auto step16 = [&](int ao, int bo) {
+    u32x4 a[RB][3];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        a[rb][pl] = *reinterpret_cast<const u32x4*>(smem + ao + pl * C::A_PLANE + rb * 16 * C::AROW);
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      u32x4 b[3];
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        b[pl] = *reinterpret_cast<const u32x4*>(smem + baddr(cb, bo) + pl * C::B_PLANE);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) bs_mac16<NP>(acc[rb][cb], a[rb], b, mfma16_bf16);
+    }
+  };
+  auto step8 = [&](int ao, int bo) {
+    u32x2 a[RB][3];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        a[rb][pl] = *reinterpret_cast<const u32x2*>(smem + ao + pl * C::A_PLANE + rb * 16 * C::AROW);
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      u32x2 b[3];
+#pragma unroll
+      for (int pl = 0; pl < C::NPL; ++pl)
+        b[pl] = *reinterpret_cast<const u32x2*>(smem + baddr(cb, bo) + pl * C::B_PLANE);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) bs_mac16<NP>(acc[rb][cb], a[rb], b, mfma16k16_bf16);
+    }
+  };
+
+  constexpr int TP = C::TH * C::TW;
+  const bool has_scale = epi.scale != nullptr;
+  WS_STAMP_DECL;
+  int k = 0;
+  for (; k < n_mine; ++k) {
+    const WsItem it = item(vidx(k));
+    float* bias_s = reinterpret_cast<float*>(smem + 2 * C::BUF) + (k & 1) * 2 * C::BM;
+    float* scale_s = bias_s + C::BM;
+    if (tid < C::BM) {
+      const int co = min(it.m0 + tid, Cout - 1);
+      bias_s[tid] = epi.bias ? epi.bias[co] : 0.f;
+      scale_s[tid] = epi.scale ? epi.scale[co] : 1.f;
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    WS_STAMP(6);
+    __syncthreads();
+    int c = it.c_begin;
+    const int c_end = it.c_end;
+    for (; c + 1 < c_end; c += 2) {
+      WS_STAMP(-1);
+      step16(aoff[0], boff[0]);
+      step16(aoff[1], boff[1]);
+      WS_STAMP(0);
+      __syncthreads();  // chunk c+1 visible
+      WS_STAMP(1);
+      step16(aoff[2], boff[2]);
+      WS_STAMP(2);
+      __syncthreads();  // buffer 0 retired
+      WS_STAMP(3);
+      step16(aoff[3], boff[3]);
+      step8(aoff4, boff4);
+      WS_STAMP(4);
+      __syncthreads();
+      WS_STAMP(5);
+    }
+    if (c < c_end) {
+      step16(aoff[0], boff[0]);
+      step16(aoff[1], boff[1]);
+      step8(aoffL, boffL);
+      __syncthreads();
+    }
+
+    // epilogue: the lane holds rows 4g..4g+3 of column l16 of each 16 x 16 tile
+    if (!it.direct) {
+      float* St = slab + ((size_t)it.split * n_tail + it.ti) * C::BM * TP;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
+            St[ml * TP + (wn * NJ + (cb >> 1)) * C::TW + (cb & 1) * 16 + l16] = acc[rb][cb][r];
+          }
+      WS_STAMP(7);
+      continue;
+    }
+    bool pooled = false;
+    if constexpr (NJ == 2) {
+      if (epi.pool) {
+        // max_pool2d(2, 2) window: pixel rows j = 0, 1 (column blocks hh and 2 + hh), columns
+        // (l16, l16 ^ 1); torch's window order and update rule, as conv_fwd_bs_kernel
+        pooled = true;
+        const int Hp = H / 2, Wp2 = W / 2;
+        float* Pn = epi.pool + (size_t)it.n * Cout * Hp * Wp2;
+        const int hp = (it.h0 + wn * NJ) / 2;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int wp = (it.w0 + hh * 16 + l16) / 2;
+          const bool writer = (l16 & 1) == 0 && hp < Hp && wp < Wp2;
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
+              float v2[2];
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                v2[j] = acc[rb][j * 2 + hh][r];
+                if (has_scale) v2[j] *= scale_s[ml];
+                v2[j] += bias_s[ml];
+                if (epi.relu) v2[j] = fmaxf(v2[j], 0.f);
+              }
+              const float c0 = __shfl_xor(v2[0], 1), c1 = __shfl_xor(v2[1], 1);
+              float m = v2[0];
+              if (c0 > m || __builtin_isnan(c0)) m = c0;
+              if (v2[1] > m || __builtin_isnan(v2[1])) m = v2[1];
+              if (c1 > m || __builtin_isnan(c1)) m = c1;
+              if (writer && it.m0 + ml < Cout) Pn[((size_t)(it.m0 + ml) * Hp + hp) * Wp2 + wp] = m;
+            }
+        }
+      }
+    }
+    if (!pooled) {
+      float* Yn = Y + (size_t)it.n * Cout * HWi;
+      const float* Rn = epi.residual ? epi.residual + (size_t)it.n * Cout * HWi : nullptr;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          const int h = it.h0 + wn * NJ + (cb >> 1), w = it.w0 + (cb & 1) * 16 + l16;
+          if (h >= H || w >= W) continue;
+          const int pix = h * W + w;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
+            const int co = it.m0 + ml;
+            if (co < Cout) {
+              const size_t idx = (size_t)co * HWi + pix;
+              float val = acc[rb][cb][r];
+              if (has_scale) val *= scale_s[ml];
+              val += bias_s[ml];
+              if (Rn) val += Rn[idx];
+              if (epi.relu) val = fmaxf(val, 0.f);
+              Yn[idx] = val;
+            }
+          }
+        }
+    }
+    WS_STAMP(7);
+  }
+  WS_STAMP_SAVE;
 }
 
 // Packed, pre-split weights for conv_fwd_bs_kernel: three bf16 planes (hi, mid, lo of the
@@ -1463,11 +1989,28 @@ static bool use_band(int H, int W) {
   return utilb > util2d * 1.05;
 }
 
+// Warp-specialized forward kernel (conv_fwd_bs_ws_kernel) instead of conv_fwd_bs_kernel.
+static bool use_ws() {
+  static const bool ws = tune_knob("TLOD_CONV_WS", 0) != 0;
+  return ws;
+}
+
+template <int WM, int WN, int MI, int NJ, int NP>
+static int ws_slots() {
+  static const int slots = resident_slots(conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>,
+                                          WM * WN * 64 + kProdWaves * 64,
+                                          WsCfg<WM, WN, MI, NJ, NP>::LDS_BYTES);
+  return slots;
+}
+
 template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
 static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_split = true) {
   using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
-  static const int slots = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>, C::NT,
-                                          C::LDS_BYTES);
+  static const int slots_plain = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>,
+                                                C::NT, C::LDS_BYTES);
+  int slots = slots_plain;
+  if constexpr (!BAND)
+    if (use_ws()) slots = ws_slots<WM, WN, MI, NJ, NP>();
   const int nchunks = div_up(Cin, C::CK);
   // cost model in f32-MFMA-equivalent time: the split products run ~16/NP x faster
   const int tw = BAND ? div_up(H * W, C::TH * C::TW) : div_up(W, C::TW);
@@ -1489,15 +2032,38 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
     set_error("tlod_conv_bs: workspace too small for split-K");
     return kWorkspace;
   }
-  const size_t lds = C::LDS_BYTES;
-  auto kern = conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>;
-  static bool attr = false;
-  if (!attr) {
-    TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
+  bool launched = false;
+  if constexpr (!BAND) {
+    // persistent warp-specialized kernel: at most one workgroup per slot (32-bit buffer
+    // offsets into one image and into the weight pack)
+    if (use_ws() && (size_t)Cin * H * W * 4 < (1ull << 31)) {
+      using WC = WsCfg<WM, WN, MI, NJ, NP>;
+      auto kern = conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>;
+      static bool attr = false;
+      if (!attr) {
+        TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)WC::LDS_BYTES));
+        attr = true;
+      }
+      static const bool one_item = tune_knob("TLOD_WS_ONE_ITEM", 0) != 0;  // A/B: no persistence
+      const long long grid = one_item ? nwg : std::min<long long>(nwg, ws_slots<WM, WN, MI, NJ, NP>());
+      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C::NT + kProdWaves * 64), WC::LDS_BYTES,
+                         s, X, Wp, epi, Y, N, Cin, H, W, Cout, p.tiles_m, p.tiles_w, p.tiles_h,
+                         p.dp_tiles, p.ksplit, p.cps, slab);
+      launched = true;
+    }
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wp, epi, Y, N, Cin, H, W,
-                     Cout, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps, slab);
+  if (!launched) {
+    const size_t lds = C::LDS_BYTES;
+    auto kern = conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>;
+    static bool attr = false;
+    if (!attr) {
+      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wp, epi, Y, N, Cin, H, W,
+                       Cout, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps, slab);
+  }
   TLOD_LAUNCH_CHECK();
   if (p.ksplit > 1) {
     const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
@@ -1666,6 +2232,16 @@ static int with_wgrad_bs_cfg(int KS, int nprod, F&& f) {
 }  // namespace tlod
 
 using namespace tlod;
+
+#if TLOD_WS_STAMPS
+extern "C" int tlod_debug_ws_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_stamps), sizeof(g_ws_stamps)) == hipSuccess &&
+                 hipMemcpyFromSymbol(host + 256 * 12 * 8, HIP_SYMBOL(g_ws_clock),
+                                     sizeof(g_ws_clock)) == hipSuccess
+             ? 0
+             : 1;
+}
+#endif
 
 extern "C" int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
                                       tlod_stream_t stream) {
