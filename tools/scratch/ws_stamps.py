@@ -19,19 +19,19 @@ wk = tc.pack_bs(w, False)
 for _ in range(30):
     tc.conv_fwd(x, w, b, True, wk=wk, math="bf16x6")
 torch.cuda.synchronize()
-buf = np.zeros(256 * 12 * 8 + 512, np.uint64)
+buf = np.zeros(256 * 12 * 10 + 512, np.uint64)
 f = _lib.lib().tlod_debug_ws_stamps
 f.argtypes = [ctypes.c_void_p]
 assert f(buf.ctypes.data) == 0
-a = buf[:256 * 12 * 8].reshape(256, 12, 8).astype(np.float64)
+a = buf[:256 * 12 * 10].reshape(256, 12, 10).astype(np.float64)
 names = ["work A (steps 0-1 / store c+1)", "wait B1", "step 2 / idle", "wait B2",
-         "work C (steps 3-4 / store c+2)", "wait B3", "pre-item | prod: store part", "epilogue | prod: load issue"]
+         "work C (steps 3-4 / store c+2)", "wait B3", "pre-item | prod: store part", "epilogue | prod: load issue", "B0 wait | prod: item prologue", "lone chunk | prod: B0 wait"]
 for role, sl in (("MFMA waves", slice(0, 8)), ("producer waves", slice(8, 12))):
     v = a[:, sl, :]
     tot = v.sum(-1)
     print(f"{role}: total cycles per wave median {np.median(tot):.0f}")
     for k, nm in enumerate(names):
         print(f"   {nm:34s} median {np.median(v[:, :, k]):10.0f}  frac {np.median(v[:, :, k] / tot):.3f}")
-clk = buf[256 * 12 * 8:].reshape(256, 2).astype(np.float64)
+clk = buf[256 * 12 * 10:].reshape(256, 2).astype(np.float64)
 print("block-0 wave-0 span: cycles %.0f, realtime %.0f us, clock %.3f GHz (median over blocks %.3f)" % (
     clk[0, 0], clk[0, 1] / 100.0, clk[0, 0] / clk[0, 1] / 10.0, np.median(clk[:, 0] / clk[:, 1] / 10.0)))
