@@ -84,8 +84,13 @@ def test_roi_align_fwd_bwd(B, C, H, W, R, ah, aw):
     np.testing.assert_allclose(ft.grad.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("B,C,H,W,R", [(1, 512, 37, 62, 256), (1, 100, 37, 75, 300), (2, 64, 12, 16, 33)])
+@pytest.mark.parametrize("B,C,H,W,R", [(1, 512, 37, 62, 256), (1, 100, 37, 75, 300), (2, 64, 12, 16, 33),
+                                       (2, 33, 37, 75, 556), (2, 8, 100, 120, 60)])
 def test_roi_align_avg_fused(B, C, H, W, R):
+    """Odd C, RoIs of two images interleaved; (2, 33, 37, 75, 556) is the DAF step's RoI
+    count on its base-feature map (the opt-in LDS-accumulation backward, TLOD_ROI_BWD_LDS=1,
+    passed these cases too; (2, 8, 100, 120) is beyond its 64 KB and takes the atomic
+    kernels)."""
     from tlod.roi_align import RoIAlignAvg
     rng = np.random.default_rng(R)
     f = _feat(rng, B, C, H, W)
