@@ -193,12 +193,17 @@ def main():
 
     achieved, detail, conv_ms, conv_f, n_launch, dom = conv_roofline(records)
     traffic, traffic_src = measured_traffic(a)
-    dom_kernels = ("conv_fwd_bs_kernel", "conv_wgrad_bs_kernel") if dom["math"] != "f32" else \
-        ("conv_fwd_kernel", "conv_wgrad_kernel")
+    dom_kernels = ("conv_fwd_bs_kernel", "conv_fwd_bs_ws_kernel", "conv_wgrad_bs_kernel") \
+        if dom["math"] != "f32" else ("conv_fwd_kernel", "conv_wgrad_kernel")
     per_launch_pmc = None
     if traffic:
-        per_launch_pmc = round(sum(traffic["bytes_per_step_by_kernel"].get(k, 0)
-                                   for k in dom_kernels) / (dom["launches"] / a.steps))
+        by_k = traffic["bytes_per_step_by_kernel"]
+        # a PMC pass that predates a kernel of the family (e.g. the warp-specialized forward,
+        # on by default since r02's profile) cannot price this run's launches: report none
+        ws_on = dom["math"] != "f32" and os.environ.get("TLOD_CONV_WS", "1") != "0"
+        if not (ws_on and "conv_fwd_bs_ws_kernel" not in by_k):
+            per_launch_pmc = round(sum(by_k.get(k, 0) for k in dom_kernels) /
+                                   (dom["launches"] / a.steps))
     result = {
         "metric": METRIC.replace("DAF VGG16", f"{a.method.upper()} {'VGG16' if a.net == 'vgg16' else 'ResNet101'}"),
         "value": round(value, 4), "unit": "img/s", "n_gpus": world,
@@ -222,7 +227,10 @@ def main():
                      "traffic_note": "PMC HBM bytes per launch of the dominant kernels "
                                      f"({' + '.join(dom_kernels)}; FETCH_SIZE x2 + WRITE_SIZE) "
                                      "vs algorithmic bytes per launch (operands read once, "
-                                     "result written once)",
+                                     "result written once)" +
+                                     ("" if per_launch_pmc is not None or not traffic else
+                                      "; null: the committed PMC pass predates "
+                                      "conv_fwd_bs_ws_kernel"),
                      "traffic_by_kernel_per_step": (traffic or {}).get("bytes_per_step_by_kernel"),
                      "kernel": f"tlod 3x3/1x1 conv, {dom['math']} arithmetic "
                                "(the family with the most time in the step)",
