@@ -334,7 +334,11 @@ int tlod_upsample2_zero_f32(const float* dy, int N, int C, int H, int W, float* 
  * d = g' + wd*p; buf = m*buf + d; p -= lr*buf
  * (torch SGD semantics, dampening 0; buf starts at 0, so step 1 gives buf = d).
  * clip_norm <= 0 disables clipping.  partials: float[n_chunks] scratch.  norm_scale: 2
- * device floats receiving (total grad norm, applied scale).  Deterministic. */
+ * device floats receiving (total grad norm, applied scale).  Deterministic.
+ * active: NULL, or a device float; a chunk whose *active == 0 is left untouched (data
+ * parallel: the number of ranks that produced the gradient, all-reduced with it — a
+ * parameter no rank used is skipped like a None .grad in torch.optim.SGD; its gradient
+ * slot is zero, so it adds nothing to the norm). */
 typedef struct tlod_sgd_chunk {
   float* param;
   const float* grad;
@@ -342,6 +346,7 @@ typedef struct tlod_sgd_chunk {
   long long count;
   float lr;
   float weight_decay;
+  const float* active;
 } tlod_sgd_chunk;
 
 int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float grad_scale,

@@ -149,8 +149,10 @@ class OracleDAF(nn.Module):
             din, dfeat = 512, 4096
             self.splits = (10, 16, 23)  # shared frozen prefix, conv3 end, conv4 end
         else:
-            from .resnet import resnet101_parts
+            from .resnet import name_sites, resnet101_parts
             self.RCNN_base, self.RCNN_top = resnet101_parts()
+            name_sites(self.RCNN_base, self.forced, "base")
+            name_sites(self.RCNN_top, self.forced, "top")
             self.rcnn_cfg["batch"] = 128
             din, dfeat = 1024, 2048
             self.splits = (5, 5, 6)  # conv1..layer1 | layer2 | layer3

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .daf_step import OracleDAF, _GRL
+from .daf_step import OracleDAF, _GRL, forced_relu
 
 
 def drm_chunks(x, scale):
@@ -64,24 +64,28 @@ class OracleMAF(OracleDAF):
         ins.clssifer = nn.Linear(1024, 2)
         self.RCNN_instanceDA = ins
 
-    def _image_da_drm(self, m, feat):
-        """_ImageDA_drm.forward (DA.py:141-149)."""
+    def _image_da_drm(self, m, feat, lvl):
+        """_ImageDA_drm.forward (DA.py:141-149); activation sites drm{lvl} / ida{lvl}."""
         x = _GRL.apply(feat, 0.1)
-        x = drm_chunks(F.relu(m.DRM.conv_low_dim(x)), m.scale)
-        return m.Conv2(F.relu(m.Conv1(x)))
+        x = drm_chunks(forced_relu(self.forced, f"drm{lvl}", m.DRM.conv_low_dim(x)), m.scale)
+        return m.Conv2(forced_relu(self.forced, f"ida{lvl}", m.Conv1(x)))
 
     def _instance_da_w(self, x, dc_label):
-        """_InstanceDA_w.forward (DA.py:90-104), no dropout."""
+        """_InstanceDA_w.forward (DA.py:90-104), no dropout.  The detached weighting pass
+        feeds no gradient: plain ReLUs; the reversed pass has the sites ip1 / ip2."""
         m = self.RCNN_instanceDA
 
-        def mlp(v):
-            return m.clssifer(F.relu(m.dc_ip2(F.relu(m.dc_ip1(v)))))
-        score = F.softmax(mlp(x.detach().clone()), dim=1)
-        return mlp(_WGRL.apply(x, score.detach(), dc_label, 0.2))
+        def mlp(v, relu1, relu2):
+            return m.clssifer(relu2(m.dc_ip2(relu1(m.dc_ip1(v)))))
+        score = F.softmax(mlp(x.detach().clone(), F.relu, F.relu), dim=1)
+        return mlp(_WGRL.apply(x, score.detach(), dc_label, 0.2),
+                   lambda v: forced_relu(self.forced, "ip1", v),
+                   lambda v: forced_relu(self.forced, "ip2", v))
 
     @staticmethod
     def _img_nll(score, label):
-        lab = torch.full((score.shape[0], *score.shape[2:]), label, dtype=torch.long)
+        lab = torch.full((score.shape[0], *score.shape[2:]), label, dtype=torch.long,
+                         device=score.device)
         return F.nll_loss(F.log_softmax(score, 1), lab)
 
     def forward(self, batch, rng, rois_override=None):
@@ -89,14 +93,14 @@ class OracleMAF(OracleDAF):
         out = {k: d[k] for k in ("rpn_loss_cls", "rpn_loss_box", "RCNN_loss_cls", "RCNN_loss_bbox",
                                  "rois")}
         for pre, lab in (("", 1), ("t_", 0)):
-            s3 = self._image_da_drm(self.RCNN_imageDA_3, d[pre + "c3"])
-            s4 = self._image_da_drm(self.RCNN_imageDA_4, d[pre + "c4"])
+            s3 = self._image_da_drm(self.RCNN_imageDA_3, d[pre + "c3"], 3)
+            s4 = self._image_da_drm(self.RCNN_imageDA_4, d[pre + "c4"], 4)
             s5 = self._image_da(d[pre + "base"])
             img = self._img_nll(s3, lab) + self._img_nll(s4, lab) + self._img_nll(s5, lab)
             fc7 = d[pre + "fc7"]
             cls_prob = F.softmax(self.RCNN_cls_score(fc7), 1)
             logits = self._instance_da_w(torch.cat((fc7, cls_prob), 1), lab)
-            y = torch.zeros(logits.shape[0], dtype=torch.long)
+            y = torch.zeros(logits.shape[0], dtype=torch.long, device=logits.device)
             y[:256] = lab  # MAF InstanceLabelResizeLayer (lib/MAF/LabelResizeLayer.py:50-60)
             ins = F.cross_entropy(logits, y)
             key = "" if lab == 1 else "tgt_"

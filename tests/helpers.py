@@ -1,5 +1,6 @@
 """Synthetic inputs shared by the tests (seeded, reference-shaped)."""
 import numpy as np
+import torch
 
 
 def random_boxes(rng, n, W=1000, H=600, min_wh=8, max_wh=300):
@@ -94,46 +95,107 @@ VGG_TRAINABLE_CONVS = (10, 12, 14, 17, 19, 21, 24, 26, 28)
 VGG_POOL_AFTER = {14: 16, 21: 23}  # conv index -> the max-pool layer index after it
 
 
-def arm_device_taps(m):
-    """Attach act_tap lists to the device model's trainable activation sites."""
+def arm_taps(m):
+    """Attach act_tap lists to every trainable activation site of a device DAF / MAF / ATF
+    model (VGG16 or ResNet101).  Returns {oracle site: (list, kind)}; kind says how the
+    device's batched calls split into the oracle's per-image / per-RoI-set calls:
+      "map"  — batch entries of a feature map (source first), "pool" likewise plus the
+               max-pool argmax of the map, "head" — RoI rows of the detection head
+               (fc6 / fc7 / ResNet layer4), "ins" — RoI rows of the instance discriminator.
+    Site names follow the oracle: base.{relu index} (VGG), base.{i}.{block}.r1..r3
+    (ResNet layer2 / layer3), top.0.{block}.r1..r3 (ResNet layer4 head), base_t.* (ATF's
+    t branch), rpn, fc6, fc7, ida / ida3 / ida4 (image DA), drm3 / drm4 (MAF DRM), ip1, ip2."""
+    from tlod.detector.resnet import Bottleneck
     taps = {}
-    for i in VGG_TRAINABLE_CONVS:
-        m.RCNN_base[i].act_tap = taps.setdefault(f"conv{i}", [])
-    m.RCNN_rpn.RPN_Conv.act_tap = taps.setdefault("rpn", [])
-    m.RCNN_top[0].act_tap = taps.setdefault("fc6", [])
-    m.RCNN_top[3].act_tap = taps.setdefault("fc7", [])
-    if hasattr(m, "RCNN_imageDA"):
-        m.RCNN_imageDA.Conv1.act_tap = taps.setdefault("ida", [])
-        m.RCNN_instanceDA.dc_ip1.act_tap = taps.setdefault("ip1", [])
-        m.RCNN_instanceDA.dc_ip2.act_tap = taps.setdefault("ip2", [])
+
+    def add(site, mod, kind):
+        mod.act_tap = []
+        taps[site] = (mod.act_tap, kind)
+
+    def backbone(base, prefix):
+        if any(isinstance(x, Bottleneck) for x in base.modules()):
+            for i, layer in enumerate(base):
+                if not isinstance(layer, torch.nn.Sequential):
+                    continue
+                for j, blk in enumerate(layer):
+                    if not any(p.requires_grad for p in blk.parameters()):
+                        continue  # frozen layer1: no gradient flows through it
+                    blk.act_tap = {"r1": [], "r2": [], "r3": []}
+                    for r in ("r1", "r2", "r3"):
+                        taps[f"{prefix}.{i}.{j}.{r}"] = (blk.act_tap[r], "head" if prefix == "top"
+                                                         else "map")
+            return
+        for i in VGG_TRAINABLE_CONVS:
+            add(f"{prefix}.{i + 1}", base[i], "map")
+            if i in VGG_POOL_AFTER:
+                taps[f"{prefix}.{VGG_POOL_AFTER[i]}"] = (base[i].act_tap, "pool")
+
+    backbone(m.RCNN_base, "base")
+    if hasattr(m, "RCNN_base_t"):
+        backbone(m.RCNN_base_t, "base_t")
+    if any(isinstance(x, Bottleneck) for x in m.RCNN_top.modules()):
+        backbone(m.RCNN_top, "top")
+    else:
+        add("fc6", m.RCNN_top[0], "head")
+        add("fc7", m.RCNN_top[3], "head")
+    add("rpn", m.RCNN_rpn.RPN_Conv, "map")
+    if not hasattr(m, "RCNN_imageDA"):  # source-only Faster R-CNN
+        return taps
+    add("ida", m.RCNN_imageDA.Conv1, "map")
+    for lvl in (3, 4):
+        h = getattr(m, f"RCNN_imageDA_{lvl}", None)
+        if h is not None:
+            add(f"ida{lvl}", h.Conv1, "map")
+            if hasattr(h, "DRM"):
+                add(f"drm{lvl}", h.DRM.conv_low_dim, "map")
+    add("ip1", m.RCNN_instanceDA.dc_ip1, "ins")
+    add("ip2", m.RCNN_instanceDA.dc_ip2, "ins")
     return taps
+
+
+def arm_device_taps(m):
+    return arm_taps(m)
 
 
 def device_forced(taps, n_rows=None):
     """Oracle ``forced`` dict (site -> per-call masks / pool indices) from the device taps.
     Batched device tensors are split into the oracle's per-image calls (source first):
-    maps by batch entry, RoI rows at n_rows (None: one call)."""
+    maps by batch entry; RoI rows by ``n_rows`` — an int (split point of the head and the
+    instance discriminator rows, DAF / MAF), a dict {"head": [sizes], "ins": [sizes]}
+    (ATF's four RoI sets), or None (one call)."""
     import torch.nn.functional as F
 
-    def parts(t, rows):
-        t = t.detach().cpu()
-        if rows == "maps":
-            return [t[i:i + 1] for i in range(t.shape[0])]
-        return [t[:rows], t[rows:]] if rows else [t]
+    def sizes(kind):
+        if isinstance(n_rows, dict):
+            return n_rows[kind]
+        return None if n_rows is None else [n_rows]
+
+    def mask(t):
+        return t if t.dtype == torch.bool else t > 0
 
     forced = {}
-    for i in VGG_TRAINABLE_CONVS:
-        ps = parts(taps[f"conv{i}"][0], "maps")
-        forced[f"base.{i + 1}"] = [p > 0 for p in ps]
-        if i in VGG_POOL_AFTER:
-            forced[f"base.{VGG_POOL_AFTER[i]}"] = [F.max_pool2d(p, 2, 2, return_indices=True)[1]
-                                                   for p in ps]
-    for site in ("rpn", "ida"):
-        if site in taps:
-            forced[site] = [p > 0 for p in parts(taps[site][0], "maps")]
-    for site in ("fc6", "fc7", "ip1", "ip2"):
-        if site in taps:
-            forced[site] = [p > 0 for p in parts(taps[site][0], n_rows)]
+    for site, (lst, kind) in taps.items():
+        if not lst:
+            continue
+        parts = []
+        if kind in ("map", "pool"):
+            for t in lst:
+                t = t.detach().cpu()
+                parts += [t[i:i + 1] for i in range(t.shape[0])]
+        else:
+            t = torch.cat([x.detach().cpu() for x in lst], 0)
+            sz = sizes(kind)
+            if sz is None:
+                parts = [t]
+            else:
+                sz = list(sz)
+                if sum(sz) < t.shape[0]:
+                    sz.append(t.shape[0] - sum(sz))
+                parts = list(torch.split(t, sz, 0))
+        if kind == "pool":
+            forced[site] = [F.max_pool2d(p, 2, 2, return_indices=True)[1] for p in parts]
+        else:
+            forced[site] = [mask(p) for p in parts]
     return forced
 
 
@@ -177,15 +239,18 @@ def pattern_grad_bar(m, o, run, cpu_batch, taps, n_rows, own32, factor=2.0, floo
     2e-7..1.5e-6 — the printed ratios keep that gap visible.  ``run(model, batch)`` returns the oracle's total
     loss; ``own32`` is the cpu32 run's recorded pattern (the caller already ran it)."""
     import copy
-    import torch
 
     def fp64_in(pattern):
-        o64 = copy.deepcopy(o).double()
+        # torch fp64 on the GPU when there is one (native im2col + dgemm for double convs:
+        # MIOpen is fp32/16 only) — the same fp64 reference, minutes faster for ATF/R101
+        d64 = "cuda" if torch.cuda.is_available() else "cpu"
+        o64 = copy.deepcopy(o).double().to(d64)
         for p in o64.parameters():
             p.grad = None
-        b64 = tuple(t.double() if t.is_floating_point() else t for t in cpu_batch)
+        b64 = tuple((t.double() if t.is_floating_point() else t).to(d64) for t in cpu_batch)
         run_in_pattern(o64, pattern, lambda: run(o64, b64).backward())
-        return dict(o64.named_parameters())
+        return {k: p.grad.detach().cpu() if p.grad is not None else None
+                for k, p in o64.named_parameters()}
 
     og = copy.deepcopy(o).cuda()
     for p in og.parameters():
@@ -202,7 +267,7 @@ def pattern_grad_bar(m, o, run, cpu_batch, taps, n_rows, own32, factor=2.0, floo
             continue
         e = []
         for name in ("device", "cpu32", "gpu32"):
-            ref = refs[name][k].grad.double()
+            ref = refs[name][k].double()
             got = runs[name][k].grad.detach().double().cpu()
             e.append(float((got - ref).norm()) / max(float(ref.norm()), 1e-30))
         errs[k] = tuple(e)
@@ -214,5 +279,33 @@ def pattern_grad_bar(m, o, run, cpu_batch, taps, n_rows, own32, factor=2.0, floo
           "| device / max(cpu32, gpu32): median", round(ratios[len(ratios) // 2], 2),
           "max", round(worst, 2))
     assert not bad, {"violations": bad, "worst_ratio": worst}
-    _ = torch
     return errs
+
+
+# ---------------------------------------------------------------- proposal sets
+def box_iou(a, b):
+    """(n,4) x (m,4) IoU, +1 pixel convention."""
+    a, b = a.astype(np.float64), b.astype(np.float64)
+    iw = np.minimum(a[:, None, 2], b[None, :, 2]) - np.maximum(a[:, None, 0], b[None, :, 0]) + 1
+    ih = np.minimum(a[:, None, 3], b[None, :, 3]) - np.maximum(a[:, None, 1], b[None, :, 1]) + 1
+    inter = np.clip(iw, 0, None) * np.clip(ih, 0, None)
+    aa = (a[:, 2] - a[:, 0] + 1) * (a[:, 3] - a[:, 1] + 1)
+    ab = (b[:, 2] - b[:, 0] + 1) * (b[:, 3] - b[:, 1] + 1)
+    return inter / (aa[:, None] + ab[None, :] - inter)
+
+
+def assert_proposal_sets_match(dev_rois, ref_rois, key):
+    """a proposal layer's output on each side's own RPN outputs.  Near-tied
+    random-init scores can reorder the sort and move the top-N boundary, so the proposals
+    are compared as sets: >= 99.5% of each side's boxes have an IoU >= 0.999 partner on the
+    other side, and the counts agree within 0.5%."""
+    d = np.asarray(dev_rois).reshape(-1, 5)
+    r = np.asarray(ref_rois).reshape(-1, 5)
+    d = d[(d[:, 3] > d[:, 1]) | (d[:, 4] > d[:, 2])]  # drop the zero padding rows
+    r = r[(r[:, 3] > r[:, 1]) | (r[:, 4] > r[:, 2])]
+    assert len(r) > 0, key
+    assert abs(len(d) - len(r)) <= max(2, len(r) // 200), (key, len(d), len(r))
+    iou = box_iou(d[:, 1:], r[:, 1:])
+    for side, best in (("device", iou.max(1)), ("oracle", iou.max(0))):
+        frac = float((best >= 0.999).mean())
+        assert frac >= 0.995, (key, side, frac)

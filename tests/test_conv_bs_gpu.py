@@ -177,3 +177,37 @@ def test_bf16x6_as_accurate_as_f32_mfma(N, Cin, Cout, H, W):
              err(conv_dgrad(gy.to(dev), w.to(dev), math=m), ref_dx)) for m in ("f32", "bf16x6")}
     assert e["bf16x6"][0] <= 1.5 * e["f32"][0] + 1e-9, e
     assert e["bf16x6"][1] <= 1.5 * e["f32"][1] + 1e-9, e
+
+
+def test_split_bf16_huge_finite_operands():
+    """Finite operands whose round-to-nearest bf16 hi would be infinite (|x| >= 0x7f7f8000,
+    ~3.396e38) keep the truncated hi: conv fwd / dgrad / wgrad and the GEMM give
+    finite results at f32-level error instead of NaN."""
+    from tlod.conv import conv_dgrad, conv_fwd, conv_wgrad
+    from tlod.linear import gemm
+    big = 3.4e38
+    assert big > 3.3961e38 and big < torch.finfo(torch.float32).max
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(1, 16, 12, 20, generator=g)
+    x[0, 3, 4, 5], x[0, 9, 10, 17], x[0, 15, 0, 0] = big, -big, big
+    w = torch.randn(32, 16, 3, 3, generator=g) * 1e-3
+    y = conv_fwd(x.to(dev), w.to(dev), None, False, math="bf16x6")
+    assert torch.isfinite(y).all()
+    _close(y, F.conv2d(x.double(), w.double(), padding=1), "bf16x6")
+    gy = torch.randn(1, 32, 12, 20, generator=g)
+    wb = w.clone()
+    wb[5, 3, 1, 1] = -big
+    dx = conv_dgrad(gy.to(dev) * 1e-3, wb.to(dev), math="bf16x6")
+    assert torch.isfinite(dx).all()
+    _close(dx, torch.nn.grad.conv2d_input(x.shape, wb.double(), gy.double() * 1e-3, padding=1),
+           "bf16x6")
+    dw = conv_wgrad(gy.to(dev) * 1e-3, x.to(dev), 3, math="bf16x6")
+    assert torch.isfinite(dw).all()
+    _close(dw, torch.nn.grad.conv2d_weight(x.double(), (32, 16, 3, 3), gy.double() * 1e-3,
+                                           padding=1), "bf16x6")
+    A = torch.randn(40, 64, generator=g)
+    A[3, 7], A[20, 63] = big, -big
+    B = torch.randn(24, 64, generator=g) * 1e-3
+    c = gemm(A.to(dev), B.to(dev), 40, 24, 64, 1, 1, None, "bf16x6")
+    assert torch.isfinite(c).all()
+    _close(c, A.double() @ B.double().t(), "bf16x6")

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import arm_device_taps, pattern_grad_bar, record_pattern
+from helpers import arm_device_taps, assert_proposal_sets_match, pattern_grad_bar, record_pattern
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -68,17 +68,6 @@ def test_daf_losses_and_grads_match_oracle(H, W, seed):
                      cpu_batch, taps, out[7].numel(), own)
 
 
-def _iou(a, b):
-    """(n,4) x (m,4) IoU, +1 pixel convention."""
-    a, b = a.astype(np.float64), b.astype(np.float64)
-    iw = np.minimum(a[:, None, 2], b[None, :, 2]) - np.maximum(a[:, None, 0], b[None, :, 0]) + 1
-    ih = np.minimum(a[:, None, 3], b[None, :, 3]) - np.maximum(a[:, None, 1], b[None, :, 1]) + 1
-    inter = np.clip(iw, 0, None) * np.clip(ih, 0, None)
-    aa = (a[:, 2] - a[:, 0] + 1) * (a[:, 3] - a[:, 1] + 1)
-    ab = (b[:, 2] - b[:, 0] + 1) * (b[:, 3] - b[:, 1] + 1)
-    return inter / (aa[:, None] + ab[None, :] - inter)
-
-
 @pytest.mark.parametrize("H,W,seed", [(256, 384, 4), (600, 1200, 5)])
 def test_daf_proposals_without_override(H, W, seed):
     """the device's own source (TRAIN 12000 -> 2000) and target (TEST 6000 ->
@@ -96,12 +85,4 @@ def test_daf_proposals_without_override(H, W, seed):
         g, r = float(out[i]), float(ref[name])
         assert abs(g - r) <= 1e-4 * max(abs(r), 1e-3), (name, g, r)
     for key, ref_key in (("s_rois", "props"), ("t_rois", "t_props")):
-        d = m.capture[key].cpu().numpy().reshape(-1, 5)
-        r = ref[ref_key].reshape(-1, 5)
-        d = d[(d[:, 3] > d[:, 1]) | (d[:, 4] > d[:, 2])]  # drop the zero padding rows
-        r = r[(r[:, 3] > r[:, 1]) | (r[:, 4] > r[:, 2])]
-        assert abs(len(d) - len(r)) <= max(2, len(r) // 200), (key, len(d), len(r))
-        iou = _iou(d[:, 1:], r[:, 1:])
-        for side, best in (("device", iou.max(1)), ("oracle", iou.max(0))):
-            frac = float((best >= 0.999).mean())
-            assert frac >= 0.995, (key, side, frac)
+        assert_proposal_sets_match(m.capture[key].cpu().numpy(), ref[ref_key], key)

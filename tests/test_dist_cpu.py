@@ -29,8 +29,10 @@ class Net(torch.nn.Module):
         self.head2 = torch.nn.Linear(64, 7)
         self.unused = torch.nn.Linear(3, 3)  # never receives a gradient (ATF's RCNN_rpn_t)
 
-    def forward(self, x, swap):
+    def forward(self, x, swap, skip_head2=False):
         h = torch.relu(self.trunk(x))
+        if skip_head2:  # this rank's graph never reaches head2 (partial gradients)
+            return (self.head1(h) ** 2).mean()
         # the later-created branch is differentiated first: swapping the branch order swaps
         # which head's gradients are ready first
         if swap:
@@ -110,4 +112,64 @@ def test_reducer_gloo_world2():
                     p.sub_(0.1 * out[f"g0_{step}"][k])
     for k in out["w0"]:
         assert torch.equal(out["w0"][k], out["w1"][k])
+        assert torch.equal(out["w0"][k], dict(m.named_parameters())[k].detach())
+
+
+def _worker_partial(rank, world, port, out):
+    """Rank 1 never produces head2's gradients; rank 0 does."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "transfer-learning-library-for-object-detection_amd"))
+    from tlod.dist import GradBucketReducer, init_from_env
+    init_from_env(backend="gloo")
+    m = _model(seed=rank)
+    red = GradBucketReducer(m, bucket_mb=1e-4)
+    for step in range(3):
+        red.zero_grad()
+        m(_data(rank * 10 + step), swap=False, skip_head2=(rank == 1)).backward()
+        red.finish(scale=True)
+        out[f"g{rank}_{step}"] = {k: (None if p.grad is None else p.grad.clone())
+                                  for k, p in m.named_parameters() if p.requires_grad}
+        with torch.no_grad():
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.sub_(0.1 * p.grad)
+    out[f"w{rank}"] = {k: p.detach().clone() for k, p in m.named_parameters()}
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_reducer_partial_gradients_gloo_world2():
+    """A parameter that only some ranks differentiate gets the reduced gradient on every
+    rank (DataParallel sums the replicas' gradients, a missing one counting as zeros), so
+    the weights stay bit-identical; one that no rank differentiates keeps .grad None."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_partial, args=(2, port, out), nprocs=2, join=True)
+    m = _model(seed=0)
+    for step in range(3):
+        grads = []
+        for rank in range(2):
+            m.zero_grad(set_to_none=True)
+            m(_data(rank * 10 + step), swap=False, skip_head2=(rank == 1)).backward()
+            grads.append({k: p.grad.clone() for k, p in m.named_parameters()
+                          if p.requires_grad and p.grad is not None})
+        assert "head2.weight" in grads[0] and "head2.weight" not in grads[1]
+        for rank in range(2):
+            got = out[f"g{rank}_{step}"]
+            assert got["unused.weight"] is None and got["unused.bias"] is None
+            for k in grads[0]:
+                ref = (grads[0][k] + grads[1].get(k, torch.zeros_like(grads[0][k]))) * 0.5
+                assert got[k] is not None, (rank, step, k)
+                torch.testing.assert_close(got[k], ref, rtol=1e-5, atol=1e-6)
+                assert torch.equal(got[k], out[f"g0_{step}"][k])
+        with torch.no_grad():
+            for k, p in m.named_parameters():
+                if k in grads[0]:
+                    p.sub_(0.1 * out[f"g0_{step}"][k])
+    for k in out["w0"]:
+        assert torch.equal(out["w0"][k], out["w1"][k]), k
         assert torch.equal(out["w0"][k], dict(m.named_parameters())[k].detach())

@@ -103,3 +103,52 @@ def test_daf_vgg16_data_parallel_two_ranks(tmp_path):
             ref = p.detach().cpu()
             assert torch.equal(ref, r0[f"w{step + 1}"][k]), (step, k,
                                                               (ref - r0[f"w{step + 1}"][k]).abs().max())
+
+
+def _worker_partial(rank, world, port, outdir):
+    """Toy model on cuda:0, fused SGD: rank 1 never differentiates head2, and no rank
+    differentiates `unused` (weight decay must not touch it)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    from tlod.dist import GradBucketReducer
+    from tlod.optim import FusedSGDClip
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(rank)
+    m = torch.nn.ModuleDict({"trunk": torch.nn.Linear(32, 64), "head1": torch.nn.Linear(64, 48),
+                             "head2": torch.nn.Linear(64, 7), "unused": torch.nn.Linear(3, 3)}).to(dev)
+    opt = FusedSGDClip([{"params": list(m.parameters()), "lr": 0.1, "weight_decay": 1e-2}],
+                       momentum=0.9, clip_norm=10.0)
+    red = GradBucketReducer(m, bucket_mb=1e-4)
+    w0 = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    for step in range(3):
+        opt.zero_grad()
+        red.zero_grad()
+        g = torch.Generator().manual_seed(100 + 10 * rank + step)
+        h = torch.relu(m["trunk"](torch.randn(16, 32, generator=g).to(dev)))
+        loss = (m["head1"](h) ** 2).mean()
+        if rank == 0:
+            loss = loss + (m["head2"](h) ** 2).mean()
+        loss.backward()
+        red.finish()
+        opt.step(grad_scale=red.grad_scale)
+    torch.cuda.synchronize()
+    torch.save({"w0": w0, "w": {k: v.detach().cpu().clone() for k, v in m.named_parameters()}},
+               os.path.join(outdir, f"p{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_fused_sgd_partial_gradients_two_ranks(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker_partial, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "p0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "p1.pt", weights_only=True)
+    for k in r0["w"]:
+        assert torch.equal(r0["w"][k], r1["w"][k]), k
+    # head2 was updated (rank 0's gradient reached rank 1), unused was not touched at all
+    assert not torch.equal(r0["w"]["head2.weight"], r0["w0"]["head2.weight"])
+    assert torch.equal(r0["w"]["unused.weight"], r0["w0"]["unused.weight"])
+    assert torch.equal(r0["w"]["unused.bias"], r0["w0"]["unused.bias"])

@@ -27,7 +27,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // then have random signs — a truncating split makes every remainder carry the sign of its
 // operand, so every dropped term has the sign of its product and the sums shrink
 // systematically (~3e-8 relative per product, a coherent bias that weight gradients
-// accumulate instead of averaging out).
+// accumulate instead of averaging out).  Finite operands of magnitude >= 0x7f7f8000 (whose
+// hi would round to infinity) fall back to the truncated hi, which is exact for every
+// finite float.
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
@@ -42,6 +44,14 @@ template <int NPL>
 __device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m,
                                        unsigned& l) {
   h = cvt_pk_bf16(x0, x1);
+  // |x| >= 0x7f7f8000 rounds up to bf16 infinity; such finite operands keep the
+  // truncated (exact) hi, so the remainders stay finite (NaN / inf pass through as is)
+  if (__builtin_expect(((h & 0x7f80u) == 0x7f80u) | ((h & 0x7f800000u) == 0x7f800000u), 0)) {
+    const unsigned t0 = __builtin_isfinite(x0) ? (__float_as_uint(x0) >> 16) : (h & 0xffffu);
+    const unsigned t1 = __builtin_isfinite(x1) ? (__float_as_uint(x1) & 0xffff0000u)
+                                               : (h & 0xffff0000u);
+    h = t0 | t1;
+  }
   const float r0 = x0 - bf_lo(h), r1 = x1 - bf_hi(h);
   m = cvt_pk_bf16(r0, r1);
   if constexpr (NPL == 3) l = cvt_pk_bf16(r0 - bf_lo(m), r1 - bf_hi(m));

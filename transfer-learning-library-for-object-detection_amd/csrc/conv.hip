@@ -1998,9 +1998,11 @@ static bool use_band(int H, int W) {
 // Warp-specialized forward for 2D tiles with >= 16 input-channel chunks (Cin >= 128):
 // measured 5-8% faster on conv3/conv4 fwd and dgrad, ~2% slower at Cin = 64 (4 chunk pairs
 // per tile: the per-tile prologue dominates).  TLOD_CONV_WS=0 disables it.
-static bool use_ws(int Cin) {
+// One predicate for the plan (resident slots) and the launch.  Only the raw-buffer-load
+// build (TLOD_WS_FLAT == 0) has 32-bit offsets into one image.
+static bool use_ws(int Cin, int H, int W) {
   static const bool ws = tune_knob("TLOD_CONV_WS", 1) != 0;
-  return ws && Cin >= 128;
+  return ws && Cin >= 128 && (TLOD_WS_FLAT != 0 || (size_t)Cin * H * W * 4 < (1ull << 31));
 }
 
 template <int WM, int WN, int MI, int NJ, int NP>
@@ -2018,7 +2020,7 @@ static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_sp
                                                 C::NT, C::LDS_BYTES);
   int slots = slots_plain;
   if constexpr (!BAND)
-    if (use_ws(Cin)) slots = ws_slots<WM, WN, MI, NJ, NP>();
+    if (use_ws(Cin, H, W)) slots = ws_slots<WM, WN, MI, NJ, NP>();
   const int nchunks = div_up(Cin, C::CK);
   // cost model in f32-MFMA-equivalent time: the split products run ~16/NP x faster
   const int tw = BAND ? div_up(H * W, C::TH * C::TW) : div_up(W, C::TW);
@@ -2042,9 +2044,8 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
   }
   bool launched = false;
   if constexpr (!BAND) {
-    // persistent warp-specialized kernel: at most one workgroup per slot (32-bit buffer
-    // offsets into one image and into the weight pack)
-    if (use_ws(Cin) && (size_t)Cin * H * W * 4 < (1ull << 31)) {
+    // warp-specialized kernel (persistent: at most one workgroup per slot)
+    if (use_ws(Cin, H, W)) {
       using WC = WsCfg<WM, WN, MI, NJ, NP>;
       // persistent (TLOD_WS_PERSIST=1) or one work item per workgroup (default: measured
       // faster — an exiting workgroup's output stores drain while the next one stages)

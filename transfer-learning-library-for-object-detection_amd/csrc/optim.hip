@@ -14,6 +14,8 @@
 
 namespace tlod {
 
+static_assert(sizeof(tlod_sgd_chunk) == 48, "descriptor layout (tlod/optim.py _DESC)");
+
 // 16-B vector path when the chunk's pointers are 16-B aligned and its count a multiple of
 // 4 (the grads can be views into the DP reducer's flat buckets at any float offset).
 __device__ __forceinline__ bool vec4_ok(const void* a, const void* b, const void* c,
@@ -78,6 +80,7 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
                                                          const float* __restrict__ norm_scale,
                                                          float gs, float momentum) {
   const tlod_sgd_chunk c = chunks[blockIdx.x];
+  if (c.active != nullptr && *c.active == 0.f) return;  // no rank produced this gradient
   const float scale = norm_scale[1];
   if (vec4_ok(c.grad, c.param, c.momentum_buf, c.count)) {
     const float4* __restrict__ g4 = reinterpret_cast<const float4*>(c.grad);

@@ -131,15 +131,21 @@ class _InstanceDA_w(nn.Module):
         self.dc_relu2 = nn.ReLU()
         self.clssifer = nn.Linear(1024, 2)
 
-    def _mlp(self, x):
-        return self.clssifer(self.dc_relu2(self.dc_ip2(self.dc_relu1(self.dc_ip1(x)))))
+    def _mlp(self, x, tap=False):
+        h = self.dc_relu1(self.dc_ip1(x))
+        if tap and getattr(self.dc_ip1, "act_tap", None) is not None:  # tests
+            self.dc_ip1.act_tap.append(h.detach().clone())
+        h = self.dc_relu2(self.dc_ip2(h))
+        if tap and getattr(self.dc_ip2, "act_tap", None) is not None:
+            self.dc_ip2.act_tap.append(h.detach().clone())
+        return self.clssifer(h)
 
     def forward(self, x, need_backprop):
         dom = _row_domain(need_backprop, x.shape[0])
         with torch.no_grad():  # x1 = torch.tensor(x): a detached pass (DA.py:91-94)
             score = F.softmax(self._mlp(x), dim=1)
             w = score.gather(1, dom.view(-1, 1)).view(-1)
-        x = self._mlp(wgrad_reverse(x, w))
+        x = self._mlp(wgrad_reverse(x, w), tap=True)
         return x, instance_label_w(x.shape[0], need_backprop.view(-1)[:1])
 
 

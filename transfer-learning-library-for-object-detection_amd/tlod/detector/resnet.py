@@ -91,14 +91,21 @@ class Bottleneck(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
+        self.act_tap = None  # tests: {"r1"|"r2"|"r3": list} receiving each ReLU's mask (NCHW)
+
+    def _tap(self, tag, y, nhwc=False):
+        if self.act_tap is not None:
+            m = y.detach() > 0
+            self.act_tap[tag].append(m.permute(0, 3, 1, 2) if nhwc else m)
+        return y
 
     def forward(self, x):
         xs = Subsample2Function.apply(x) if self.stride == 2 else x
-        out = conv_bn(xs, self.conv1, self.bn1, relu=True)
-        out = conv_bn(out, self.conv2, self.bn2, relu=True)
+        out = self._tap("r1", conv_bn(xs, self.conv1, self.bn1, relu=True))
+        out = self._tap("r2", conv_bn(out, self.conv2, self.bn2, relu=True))
         res = (conv_bn(xs, self.downsample[0], self.downsample[1], relu=False)
                if self.downsample is not None else x)
-        return conv_bn(out, self.conv3, self.bn3, relu=True, residual=res)
+        return self._tap("r3", conv_bn(out, self.conv3, self.bn3, relu=True, residual=res))
 
     # ---------------------------------------------------------------- RoI head path
     @staticmethod
@@ -123,13 +130,15 @@ class Bottleneck(nn.Module):
         xm = x.reshape(R * H * W, C)
         out = self._gemm_bn(xm, self.conv1, self.bn1, relu=True)
         P = out.shape[1]
+        self._tap("r1", out.view(R, H, W, P), nhwc=True)
         pad = F.pad(out.view(R, H, W, P), (0, 0, 1, 1, 1, 1))
         taps = torch.cat([pad[:, kh:kh + H, kw:kw + W, :] for kh in range(3) for kw in range(3)], 3)
         out = self._gemm_bn(taps.reshape(R * H * W, 9 * P), self.conv2, self.bn2, relu=True)
+        self._tap("r2", out.view(R, H, W, P), nhwc=True)
         res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False)
                if self.downsample is not None else xm)
         out = self._gemm_bn(out, self.conv3, self.bn3, relu=True, residual=res)
-        return out.view(R, H, W, -1)
+        return self._tap("r3", out.view(R, H, W, -1), nhwc=True)
 
 
 class ResNetBase(nn.Sequential):

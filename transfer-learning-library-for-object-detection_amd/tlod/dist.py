@@ -63,8 +63,12 @@ class GradBucketReducer:
         if arena is None:
             arena = arena_of(params[0]) if params else None
             if arena is None or set(arena.params) != set(params):
-                n = len(params)
-                arena = GradArena(params, order=range(n - 1, -1, -1))
+                arena = GradArena(params)
+        # first-step bucket order: reverse registration (the heads' gradients are ready
+        # first), also when the arena was created by the optimizer in forward order; the
+        # tail holds one gradient-producer count per parameter (see finish())
+        n = len(arena.params)
+        arena.layout(range(n - 1, -1, -1), tail=n)
         self.arena = arena
         self.cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         self.relayout_pending = relayout
@@ -88,6 +92,9 @@ class GradBucketReducer:
             end = off + n
         if cur:
             self.buckets.append({"params": cur, "lo": start, "hi": end})
+        # the producer-count tail rides on the last bucket (contiguous with it), which
+        # therefore launches from finish() once every rank knows its own set
+        self.buckets[-1]["hi"] = a.tail_off + a.tail_len
         for bi, b in enumerate(self.buckets):
             for p in b["params"]:
                 self.bucket_of[p] = bi
@@ -111,7 +118,7 @@ class GradBucketReducer:
     def _launch_ready_prefix(self):
         while self.next < len(self.buckets):
             b = self.buckets[self.next]
-            if b["ready"] != len(b["params"]):
+            if b["ready"] != len(b["params"]) + (self.next == len(self.buckets) - 1):
                 return
             b["work"] = dist.all_reduce(self._flat(b), op=dist.ReduceOp.SUM, group=self.group,
                                         async_op=True)
@@ -129,23 +136,50 @@ class GradBucketReducer:
         self._launch_ready_prefix()
 
     def finish(self, scale=False):
-        """Launch what is left (in list order) and wait.  A parameter that got no gradient
-        this step contributes zeros (its .grad stays None, as with set_to_none).
-        scale=True: divide the gradients by the world size here (for optimizers that take
-        no grad_scale)."""
+        """Launch what is left (in list order) and wait.
+
+        A parameter this rank gave no gradient contributes zeros.  Every rank writes 1 into
+        the parameter's producer-count slot (arena tail) when it did produce the gradient,
+        and the count is summed with the last bucket, so all ranks agree on which
+        parameters were used anywhere (DataParallel's Broadcast backward sums the replicas'
+        gradients, treating a missing one as zeros):
+          * used on some rank: .grad is the reduced slot on every rank (also where this rank
+            produced none — without this, that rank would skip its update and the weights
+            and clip norm would diverge silently);
+          * used on no rank: the fused optimizer skips it on the device (count 0), as
+            torch.optim.SGD skips a None gradient; with scale=True (host optimizers) the
+            counts are read back and such gradients are set to None.
+        scale=True: also divide the gradients by the world size here (for optimizers that
+        take no grad_scale)."""
+        a = self.arena
+        unmarked = [p for p in a.params if p not in self.marked]
         for b in self.buckets[self.next:]:
             for p in b["params"]:
                 if p not in self.marked:
-                    self.arena.view(p).zero_()
+                    a.view(p).zero_()
             b["ready"] = len(b["params"])
+        if unmarked:
+            m = torch.ones(len(a.params), dtype=torch.float32)
+            for p in unmarked:
+                m[a.index[p]] = 0.0
+            a.active.copy_(m)
+        else:
+            a.active.fill_(1.0)
+        self.buckets[-1]["ready"] += 1
         self._launch_ready_prefix()
         for b in self.buckets:
             b["work"].wait()
+        for p in unmarked:
+            p.grad = a.view(p)
         seen = self.seen
         if self.relayout_pending:
             self._relayout(seen)
         if scale:
-            self.arena.flat.mul_(self.grad_scale)
+            a.flat[:a.tail_off].mul_(self.grad_scale)
+            used = (a.active > 0).tolist()
+            for p in a.params:
+                if not used[a.index[p]]:
+                    p.grad = None
         self._reset()
         return seen
 
@@ -159,5 +193,5 @@ class GradBucketReducer:
         t = torch.tensor(order, dtype=torch.int64, device=dev)
         dist.broadcast(t, dist.get_global_rank(self.group, 0) if self.group else 0,
                        group=self.group)
-        self.arena.layout(t.cpu().tolist())
+        self.arena.layout(t.cpu().tolist())  # moves the gradients and the counts along
         self._build_buckets()

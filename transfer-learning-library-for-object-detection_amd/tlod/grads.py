@@ -16,7 +16,10 @@ gradient addresses move or cost a zero fill.  Here:
     place.
 
 Semantics stay those of ``zero_grad(set_to_none=True)``: a parameter that receives no
-gradient in a step keeps ``.grad = None`` (torch.optim.SGD then skips it).
+gradient in a step keeps ``.grad = None`` (torch.optim.SGD then skips it).  Under data
+parallelism the reducer (tlod.dist) extends the arena by a tail of one float per parameter
+(``tail``/``active``): the number of ranks that produced the parameter's gradient, summed by
+the same all-reduce as the gradients, which the fused optimizer reads on the device.
 """
 import torch
 
@@ -41,20 +44,30 @@ class GradArena:
         self.gen = 0
         self._claimed = {}
         self.listeners = []
+        self.tail_len = 0
+        self.active = None  # per-parameter gradient-producer counts (tail view), DP only
         self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self.layout(order if order is not None else range(len(params)))
 
-    def layout(self, order):
-        """(Re)assign slots in the given parameter order; existing gradients move along."""
+    def layout(self, order, tail=None):
+        """(Re)assign slots in the given parameter order (indices into ``params``); existing
+        gradients move along.  tail: floats reserved after the last slot (kept if None)."""
         order = [self.params[i] for i in order]
         assert len(order) == len(self.params) and len(set(order)) == len(order)
+        if tail is not None:
+            self.tail_len = _pad(int(tail))
         offs, off = {}, 0
         for p in order:
             offs[p] = off
             off += _pad(p.numel())
-        flat = torch.zeros(off, dtype=torch.float32, device=self.params[0].device)
-        old = getattr(self, "flat", None)
+        self.tail_off = off
+        flat = torch.zeros(off + self.tail_len, dtype=torch.float32,
+                           device=self.params[0].device)
+        old, old_active = getattr(self, "flat", None), getattr(self, "active", None)
         self.order, self.offset, self.flat = order, offs, flat
+        self.active = self.flat.narrow(0, off, len(self.params)) if self.tail_len else None
+        if old_active is not None and self.active is not None:
+            self.active.copy_(old_active)
         for p in order:
             p._tlod_grad_arena = self
             if old is not None and p.grad is not None:

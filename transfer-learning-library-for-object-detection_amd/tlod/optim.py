@@ -17,7 +17,9 @@ from .grads import GradArena, arena_of
 
 CHUNK = 65536
 _DESC = np.dtype([("param", np.uint64), ("grad", np.uint64), ("buf", np.uint64),
-                  ("count", np.int64), ("lr", np.float32), ("wd", np.float32)])
+                  ("count", np.int64), ("lr", np.float32), ("wd", np.float32),
+                  ("active", np.uint64)])
+assert _DESC.itemsize == 48  # sizeof(tlod_sgd_chunk), include/tlod.h
 
 
 class FusedSGDClip:
@@ -62,8 +64,10 @@ class FusedSGDClip:
         """Descriptor rows for every parameter that has a gradient (torch.optim.SGD skips
         the others entirely: no weight decay, no momentum update)."""
         grads = [p.grad for p in self.params]
+        a = self.arena
+        act = a.active if a is not None and a.active is not None else None
         key = tuple(0 if g is None else g.data_ptr() for g in grads) + \
-            tuple(g["lr"] for g in self.param_groups)
+            tuple(g["lr"] for g in self.param_groups) + (0 if act is None else act.data_ptr(),)
         hit = self._tables.get(key)
         if hit is not None:
             self._n = hit[1]
@@ -78,10 +82,12 @@ class FusedSGDClip:
                     continue
                 assert gr.is_contiguous() and p.is_contiguous()
                 n = p.numel()
+                # data parallel: skipped on the device when no rank produced the gradient
+                ap = 0 if act is None else act.data_ptr() + 4 * a.index[p]
                 for off in range(0, n, CHUNK):
                     rows.append((p.data_ptr() + 4 * off, gr.data_ptr() + 4 * off,
                                  buf.data_ptr() + 4 * off, min(CHUNK, n - off), g["lr"],
-                                 g.get("weight_decay", 0.0)))
+                                 g.get("weight_decay", 0.0), ap))
                 idx += 1
         arr = np.array(rows, dtype=_DESC)
         table = torch.empty(arr.nbytes, dtype=torch.uint8, device=self.partials.device)
