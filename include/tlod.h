@@ -235,7 +235,7 @@ int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float* scale, fl
 
 /* ------------------------------------------------------------------ Split-bf16 3x3 conv
  * The forward / dgrad of tlod_conv_fwd_f32 on the bf16 MFMA: each f32 operand is split
- * exactly into three bf16 terms (x = hi + mid + lo, truncation) and nprod = 6 products
+ * exactly into three bf16 terms (x = hi + mid + lo, round-to-nearest) and nprod = 6 products
  * (hi*hi, hi*mid, mid*hi, hi*lo, mid*mid, lo*hi) are accumulated in f32 — error at the
  * level of f32 rounding (normwise ~1e-7 vs fp64, like the f32-input MFMA path) at up to
  * 2.7x its MFMA rate; nprod = 3 (hi*hi, hi*mid, mid*hi) trades that for ~5e-6.
@@ -397,6 +397,17 @@ int tlod_space_to_depth_f32(const float* x, int B, int C, int H, int W, int scal
                             tlod_stream_t stream);
 int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int W, int scale, float* dx,
                             tlod_stream_t stream);
+/* The whole DRM forward, lib/MAF/drm.py:10-42 (conv_low_dim 1x1 without bias -> ReLU ->
+ * crop -> space-to-depth) as one conv launch whose epilogue stores each ReLU output at its
+ * space-to-depth position: x (N, Cin, H, W), wk = tlod_conv_pack_fwd_f32 of the (Cout, Cin,
+ * 1, 1) weight, y (N, Cout*s*s, H/s, W/s); the full-resolution map is never written.  ws:
+ * tlod_conv_fwd_workspace_bytes(N, Cin, H, W, Cout, 1).  tlod_drm_relu_bwd_f32 is its
+ * backward up to the conv, in one pass: g (N, Cout, H, W) = depth_to_space(dy * (y > 0))
+ * (0 on the cropped border) — the gradient that conv_low_dim's dgrad / wgrad consume. */
+int tlod_drm_fwd_f32(const float* x, const float* wk, float* y, int N, int Cin, int H, int W,
+                     int Cout, int scale, void* ws, size_t ws_bytes, tlod_stream_t stream);
+int tlod_drm_relu_bwd_f32(const float* dy, const float* y, int B, int C, int H, int W, int scale,
+                          float* g, tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ FC head activation
  * Replaces: nn.ReLU(inplace) + nn.Dropout(p) after the head's Linear layers

@@ -28,6 +28,10 @@ def _close(got, ref, math):
 SHAPES = [  # N, Cin, Cout, H, W
     (2, 64, 128, 37, 75), (1, 3, 64, 50, 70), (2, 256, 256, 30, 40), (1, 512, 512, 37, 62),
     (1, 13, 20, 9, 33), (1, 130, 132, 9, 33), (1, 64, 256, 150, 250),
+    # warp-specialized kernel (Cin >= 128) on its run-time tiles (ws_tile): 15 x 34 at
+    # 150 x 300, 13 x 39 at 75 x 150, 19 x 26 at 37 x 75, 2 x 158 rows, blocks wrapping rows
+    (2, 256, 256, 150, 300), (1, 128, 136, 75, 150), (1, 256, 64, 37, 75), (1, 128, 128, 2, 700),
+    (1, 144, 128, 61, 9),
 ]
 
 

@@ -7,7 +7,9 @@
 // Part 2: 16x16 dot products of length K (positive operands in [0, 1), and signed ones) in
 //         bf16x6 with (a) one accumulator, products in the kernels' order, (b) hi*hi in one
 //         accumulator and the five cross/low products in a second one, added at the end,
-//         (c) a plain f32 fmaf chain; mean signed and rms relative error vs fp64.
+//         (c) a plain f32 fmaf chain, (d) hi*hi on the running accumulator and each k-step's
+//         cross / low products summed from zero then added in f32, (e) each k-step's six
+//         products summed from zero then added in f32; mean signed and rms error vs fp64.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -71,12 +73,14 @@ __global__ void round_probe(const unsigned short* a, const unsigned short* b, fl
 
 // Part 2: one wave per 16x16 output tile; A: 16 x K row-major, Bt: 16 x K row-major (B^T).
 __global__ void dot_probe(const float* A, const float* Bt, int K, float* Da, float* Db,
-                          float* Dc) {
+                          float* Dc, float* Dd, float* De) {
   const int l = threadIdx.x, l16 = l & 15, g = l >> 4;
   const size_t t = blockIdx.x;
   const float* At = A + t * 16 * K;
   const float* Btt = Bt + t * 16 * K;
-  f32x4 acc = {0, 0, 0, 0}, m = {0, 0, 0, 0}, x = {0, 0, 0, 0};
+  f32x4 acc = {0, 0, 0, 0}, m = {0, 0, 0, 0}, x = {0, 0, 0, 0}, d = {0, 0, 0, 0},
+        e4 = {0, 0, 0, 0};
+  const f32x4 z = {0, 0, 0, 0};
   for (int kb = 0; kb < K; kb += 32) {
     float av[8], bv[8];
     for (int e = 0; e < 8; ++e) {
@@ -100,6 +104,23 @@ __global__ void dot_probe(const float* A, const float* Bt, int K, float* Da, flo
     x = mf(a[2], b[0], x);
     x = mf(a[1], b[1], x);
     x = mf(a[0], b[2], x);
+    // (d) hi*hi into the running accumulator, this k-step's five cross / low products
+    //     summed from zero and added with one round-to-nearest f32 add
+    f32x4 t = mf(a[1], b[0], z);
+    t = mf(a[0], b[1], t);
+    t = mf(a[2], b[0], t);
+    t = mf(a[1], b[1], t);
+    t = mf(a[0], b[2], t);
+    d = mf(a[0], b[0], d);
+    d += t;
+    // (e) the whole k-step (all six products) from zero, then one f32 add
+    f32x4 u = mf(a[1], b[0], z);
+    u = mf(a[0], b[1], u);
+    u = mf(a[2], b[0], u);
+    u = mf(a[1], b[1], u);
+    u = mf(a[0], b[2], u);
+    u = mf(a[0], b[0], u);
+    e4 += u;
   }
   // (c) f32 fmaf chain for the 4 outputs of this lane
   for (int r = 0; r < 4; ++r) {
@@ -110,6 +131,8 @@ __global__ void dot_probe(const float* A, const float* Bt, int K, float* Da, flo
     Da[o] = acc[r];
     Db[o] = m[r] + x[r];
     Dc[o] = s;
+    Dd[o] = d[r];
+    De[o] = e4[r];
   }
 }
 
@@ -159,21 +182,25 @@ int main() {
       std::vector<float> A((size_t)T * 16 * K), B((size_t)T * 16 * K);
       for (auto& v : A) v = u(rng);
       for (auto& v : B) v = u(rng);
-      float *dA, *dB, *d1, *d2, *d3;
+      float *dA, *dB, *d1, *d2, *d3, *d4, *d5;
       CK(hipMalloc(&dA, A.size() * 4));
       CK(hipMalloc(&dB, B.size() * 4));
       CK(hipMalloc(&d1, T * 256 * 4));
       CK(hipMalloc(&d2, T * 256 * 4));
       CK(hipMalloc(&d3, T * 256 * 4));
+      CK(hipMalloc(&d4, T * 256 * 4));
+      CK(hipMalloc(&d5, T * 256 * 4));
       CK(hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice));
       CK(hipMemcpy(dB, B.data(), B.size() * 4, hipMemcpyHostToDevice));
-      dot_probe<<<T, 64>>>(dA, dB, K, d1, d2, d3);
+      dot_probe<<<T, 64>>>(dA, dB, K, d1, d2, d3, d4, d5);
       CK(hipDeviceSynchronize());
-      std::vector<float> r1(T * 256), r2(T * 256), r3(T * 256);
+      std::vector<float> r1(T * 256), r2(T * 256), r3(T * 256), r4(T * 256), r5(T * 256);
       CK(hipMemcpy(r1.data(), d1, T * 256 * 4, hipMemcpyDeviceToHost));
       CK(hipMemcpy(r2.data(), d2, T * 256 * 4, hipMemcpyDeviceToHost));
       CK(hipMemcpy(r3.data(), d3, T * 256 * 4, hipMemcpyDeviceToHost));
-      double ms[3] = {0, 0, 0}, rms[3] = {0, 0, 0}, nrm = 0;
+      CK(hipMemcpy(r4.data(), d4, T * 256 * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(r5.data(), d5, T * 256 * 4, hipMemcpyDeviceToHost));
+      double ms[5] = {0, 0, 0, 0, 0}, rms[5] = {0, 0, 0, 0, 0}, nrm = 0;
       for (int t = 0; t < T; ++t)
         for (int i = 0; i < 16; ++i)
           for (int j = 0; j < 16; ++j) {
@@ -184,22 +211,27 @@ int main() {
               aref += fabs(p);
             }
             const size_t o = (size_t)t * 256 + i * 16 + j;
-            const double e[3] = {(r1[o] - ref) / aref, (r2[o] - ref) / aref, (r3[o] - ref) / aref};
-            for (int v = 0; v < 3; ++v) {
+            const double e[5] = {(r1[o] - ref) / aref, (r2[o] - ref) / aref, (r3[o] - ref) / aref,
+                                 (r4[o] - ref) / aref, (r5[o] - ref) / aref};
+            for (int v = 0; v < 5; ++v) {
               ms[v] += e[v];
               rms[v] += e[v] * e[v];
             }
             nrm += 1;
           }
       printf("part 2: K=%d operands in [%d,1): error / sum|a b|  mean-signed / rms\n", K, sign ? -1 : 0);
-      const char* nm[3] = {"one accumulator (kernel order)", "hi*hi + separate cross acc", "f32 fmaf chain"};
-      for (int v = 0; v < 3; ++v)
+      const char* nm[5] = {"one accumulator (kernel order)", "hi*hi + separate cross acc",
+                           "f32 fmaf chain", "per-k-step cross sum + f32 add",
+                           "per-k-step 6-product sum + f32 add"};
+      for (int v = 0; v < 5; ++v)
         printf("  %-32s %+.3e  %.3e\n", nm[v], ms[v] / nrm, sqrt(rms[v] / nrm));
       CK(hipFree(dA));
       CK(hipFree(dB));
       CK(hipFree(d1));
       CK(hipFree(d2));
       CK(hipFree(d3));
+      CK(hipFree(d4));
+      CK(hipFree(d5));
     }
   }
   return 0;

@@ -19,17 +19,18 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// Exact split x = hi + mid + lo into bf16 terms, each the round-to-nearest-even bf16 of
-// the remainder (v_cvt_pk_bf16_f32, two elements per instruction; element 0 in the low
-// half).  hi keeps 8 significant bits, the remainder x - hi is exact with <= 16 bits,
-// mid its RNE 8 bits and lo the exact rest (<= 8 bits).  Round-to-nearest matters for
-// accuracy, not exactness: the products the bf16x6 scheme drops (mid*lo, lo*mid, lo*lo)
-// then have random signs — a truncating split makes every remainder carry the sign of its
-// operand, so every dropped term has the sign of its product and the sums shrink
-// systematically (~3e-8 relative per product, a coherent bias that weight gradients
-// accumulate instead of averaging out).  Finite operands of magnitude >= 0x7f7f8000 (whose
-// hi would round to infinity) fall back to the truncated hi, which is exact for every
-// finite float.
+// Exact split x = hi + mid + lo into bf16 terms: hi = the truncated top 8 significant bits
+// (exact and finite for every finite x), mid and lo the round-to-nearest-even bf16 of the
+// remainders (v_cvt_pk_bf16_f32, two elements per instruction; element 0 in the low half).
+// The remainder x - hi is exact with <= 16 bits, mid keeps its top 8 (rounded) and lo the
+// exact rest (<= 8 bits).  Round-to-nearest on mid and lo matters for accuracy, not
+// exactness: the products the bf16x6 scheme drops (mid*lo, lo*mid, lo*lo) each carry a lo
+// factor of random sign — with every term truncated (round 1) each remainder had the sign
+// of its operand, every dropped term the sign of its product, and the sums shrank
+// systematically (~3e-8 relative per product).  A round-to-nearest hi (round 2) needed a
+// check for operands that round to bf16 infinity; the truncated hi needs none and costs the
+// same one instruction per pair.  NaN / infinity operands give NaN products (their
+// remainders are NaN), as the f32 MFMA path would propagate them.
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
@@ -43,16 +44,9 @@ __device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 
 template <int NPL>
 __device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m,
                                        unsigned& l) {
-  h = cvt_pk_bf16(x0, x1);
-  // |x| >= 0x7f7f8000 rounds up to bf16 infinity; such finite operands keep the
-  // truncated (exact) hi, so the remainders stay finite (NaN / inf pass through as is)
-  if (__builtin_expect(((h & 0x7f80u) == 0x7f80u) | ((h & 0x7f800000u) == 0x7f800000u), 0)) {
-    const unsigned t0 = __builtin_isfinite(x0) ? (__float_as_uint(x0) >> 16) : (h & 0xffffu);
-    const unsigned t1 = __builtin_isfinite(x1) ? (__float_as_uint(x1) & 0xffff0000u)
-                                               : (h & 0xffff0000u);
-    h = t0 | t1;
-  }
-  const float r0 = x0 - bf_lo(h), r1 = x1 - bf_hi(h);
+  const unsigned u0 = __float_as_uint(x0) & 0xffff0000u, u1 = __float_as_uint(x1) & 0xffff0000u;
+  h = (u0 >> 16) | u1;  // v_perm_b32
+  const float r0 = x0 - __uint_as_float(u0), r1 = x1 - __uint_as_float(u1);
   m = cvt_pk_bf16(r0, r1);
   if constexpr (NPL == 3) l = cvt_pk_bf16(r0 - bf_lo(m), r1 - bf_hi(m));
 }
@@ -76,28 +70,37 @@ __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
 }
 
 // One k-step of the split-bf16 product of a 32x32 tile (NP = 3 or 6 bf16 products),
-// chained into the running accumulator.  Accuracy note: the bf16 MFMA's
-// accumulation of these chains carries a small coherent shrink — measured -3e-9 relative
-// per conv layer on random data, ~-6e-8 per layer through VGG16 (none for the f32 MFMA
-// or the vendor libraries).  TLOD_BS_KSUM=1 sums each k-step's products from zero and adds
-// the sum with a VALU add (IEEE), but needs a 16-register temporary per live tile: the
-// current tilings spill with it, so it is off.
+// added to the running accumulator.  Accuracy (tools/probe/mfma_round.hip):
+// the bf16 MFMA adds its products into the accumulator with the bits below the sum's
+// precision truncated (8 products of 0.19 ulp each add nothing; one of 0.75 ulp rounds to
+// nearest), so small products chained onto a large accumulator are floored — a coherent
+// shrink (-1e-7 relative on length-4608 positive dot products, -3e-9 per conv layer on
+// random data).  TLOD_BS_KSUM=1 sums each k-step's products from zero (small first) and
+// adds that sum with one round-to-nearest f32 add: the shrink drops to -1.4e-9 and the rms
+// error to 0.3x (below the f32 fmaf chain's).  Cost: a temporary per live tile and one
+// VALU add per accumulator register per k-step.
+// Off by default: the 32x32 kernels' 16-register temporaries spill (fwd_bs 0 -> 700 VGPRs,
+// wgrad_bs 0 -> 64, gemm_bs 0 -> 21); in the warp-specialized 16x16x32 kernel
+// (TLOD_BS_KSUM16) the temporary is 4 registers, but the adds beside the producers' split
+// VALU cost the DAF step 4% (62.0 vs 64.6 img/s, one lease).
 #ifndef TLOD_BS_KSUM
 #define TLOD_BS_KSUM 0
+#endif
+#ifndef TLOD_BS_KSUM16
+#define TLOD_BS_KSUM16 0
 #endif
 template <int NP>
 __device__ __forceinline__ void bs_mac(f32x16& acc, u32x4 a0, u32x4 a1, u32x4 a2, u32x4 b0,
                                        u32x4 b1, u32x4 b2) {
   if (TLOD_BS_KSUM) {
-    f32x16 t = mfma_bf16(a0, b0, f32x16{});
-    t = mfma_bf16(a1, b0, t);
+    f32x16 t = mfma_bf16(a1, b0, f32x16{});
     t = mfma_bf16(a0, b1, t);
     if constexpr (NP == 6) {
       t = mfma_bf16(a2, b0, t);
       t = mfma_bf16(a1, b1, t);
       t = mfma_bf16(a0, b2, t);
     }
-    acc += t;
+    acc += mfma_bf16(a0, b0, t);
   } else {
     acc = mfma_bf16(a0, b0, acc);
     acc = mfma_bf16(a1, b0, acc);

@@ -21,6 +21,9 @@
 #include "bs_common.h"
 #include "tlod.h"
 
+#include <algorithm>
+#include <cmath>
+
 namespace tlod {
 
 
@@ -78,7 +81,21 @@ struct Epi {
   int relu;
   float* pool;  // conv_fwd_bs_kernel (2D tiles, no split-K) only: write max_pool2d(2, 2) of
                 // the result here (N, Cout, H/2, W/2) instead of the full map
+  int s2d;      // conv_fwd_kernel only (MAF DRM, lib/MAF/drm.py:20-42): > 1 stores the result
+                // cropped to (H/s*s, W/s*s) and space-to-depth rearranged, (N, Cout*s*s, H/s,
+                // W/s) with channel co*s*s + (h%s)*s + w%s; no residual
 };
+
+// Element offset of output (n, co, h, w) under the epilogue's store layout; -1: cropped by
+// the DRM space-to-depth.
+__device__ __forceinline__ long long epi_out_index(const Epi& e, int n, int co, int h, int w,
+                                                   int Cout, int H, int W) {
+  if (e.s2d <= 1) return (((long long)n * Cout + co) * H + h) * W + w;
+  const int s = e.s2d, Ho = H / s, Wo = W / s;
+  if (h >= Ho * s || w >= Wo * s) return -1;
+  const long long cc = ((long long)n * Cout + co) * s * s + (h % s) * s + w % s;
+  return (cc * Ho + h / s) * Wo + w / s;
+}
 
 // ======================================================================= forward
 // Block tile: BM = WM*MI*32 output channels x BN = TH*32 pixels (TH = WN*NJ rows of 32).
@@ -335,7 +352,12 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
           v += bias_s[ml];
           if (Rn) v += Rn[idx];
           if (epi.relu) v = fmaxf(v, 0.f);
-          Yn[idx] = v;
+          if (epi.s2d > 1) {
+            const long long o = epi_out_index(epi, n, co, h, w, Cout, H, W);
+            if (o >= 0) Y[o] = v;
+          } else {
+            Yn[idx] = v;
+          }
         }
       }
     }
@@ -757,12 +779,21 @@ __device__ unsigned long long g_ws_clock[512];
 // read rows r and r+4.. of two units an odd number of slots apart — conflict-free), a
 // buffer of an odd number of 16-B slots (the unit pair that straddles the two buffers stays
 // odd apart), and two (bias, scale) slots for consecutive work items.
+// The tile is TH x TW pixels chosen per map at run time (TH * TW <= 512, the 8 waves' 32
+// column blocks of 16; ws_tile()): MFMA column block cb of wave wn covers tile pixels
+// q = 64 wn + 16 cb + l16 in row-major (r, c) = (q / TW, q % TW) order, so a block may wrap a
+// row.  150x300 maps take 15 x 34 tiles (90 tiles, 2% padding) instead of 16 x 32 (100
+// tiles, 14%).  The staged patch is (TH + 2) x (TW + 2) <= kWsPos positions.
+constexpr int kWsPos = 640;
 template <int WM, int WN, int MI, int NJ, int NP>
 struct WsCfg : BsCfg<WM, WN, MI, NJ, NP, false> {
   using B = BsCfg<WM, WN, MI, NJ, NP, false>;
   static constexpr int AROW = 160;
   static constexpr int A_PLANE = B::BM * AROW;
-  static constexpr int BUF0 = B::NPL * (A_PLANE + B::B_PLANE);
+  static constexpr int TPIX = B::TH * B::TW;  // MFMA pixels per tile (512)
+  static constexpr int BPOS = kWsPos;
+  static constexpr int B_PLANE = BPOS * 16;
+  static constexpr int BUF0 = B::NPL * (A_PLANE + B_PLANE);
   static constexpr int BUF = (BUF0 / 16) % 2 == 0 ? BUF0 + 16 : BUF0;
   static constexpr int LDS_BYTES = 2 * BUF + 4 * B::BM * 4;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -779,9 +810,21 @@ __device__ __forceinline__ f32x4 mfma16k16_bf16(u32x2 a, u32x2 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(bf16x4, a),
                                                    __builtin_bit_cast(bf16x4, b), c, 0, 0, 0);
 }
-// bs_mac's product order (a0b0, a1b0, a0b1, a2b0, a1b1, a0b2) on a 16x16 tile
+// bs_mac on a 16x16 tile: the k-step's products summed from zero (small ones first), then
+// added to the running accumulator with one f32 add (TLOD_BS_KSUM16, see bs_mac)
 template <int NP, typename V, typename F>
 __device__ __forceinline__ void bs_mac16(f32x4& acc, const V (&a)[3], const V (&b)[3], F mf) {
+  if (TLOD_BS_KSUM16) {
+    f32x4 t = mf(a[1], b[0], f32x4{0.f, 0.f, 0.f, 0.f});
+    t = mf(a[0], b[1], t);
+    if constexpr (NP == 6) {
+      t = mf(a[2], b[0], t);
+      t = mf(a[1], b[1], t);
+      t = mf(a[0], b[2], t);
+    }
+    acc += mf(a[0], b[0], t);
+    return;
+  }
   acc = mf(a[0], b[0], acc);
   acc = mf(a[1], b[0], acc);
   acc = mf(a[0], b[1], acc);
@@ -829,7 +872,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     __attribute__((amdgpu_waves_per_eu(3, 3))) conv_fwd_bs_ws_kernel(
         const float* __restrict__ X, const unsigned short* __restrict__ Wp, Epi epi,
         float* __restrict__ Y, int N, int Cin, int H, int W, int Cout, int tiles_m, int tiles_w,
-        int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab) {
+        int tiles_h, int dp_tiles, int ksplit, int cps, float* __restrict__ slab, int TH, int TW) {
   using C = WsCfg<WM, WN, MI, NJ, NP>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -839,9 +882,10 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
   const int HWi = H * W;
   const int nchunks = (Cin + C::CK - 1) / C::CK;
   const int tid = threadIdx.x;
+  const int PW = TW + 2, PP = (TH + 2) * PW;  // staged patch: row pitch, positions
   auto item = [&](int v) {
     return ws_item(v, tiles_m, tiles_w, tiles_h, dp_tiles, n_tail, ksplit, cps, nchunks, C::BM,
-                   C::TH, C::TW);
+                   TH, TW);
   };
   // This workgroup's items are b, b + G, ...; odd workgroups take them in rotated order
   // (last first), so that the workgroups' epilogue store bursts do not all coincide when the
@@ -884,7 +928,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
       const int pos = ptid + i * PT;
-      b_pos[i] = pos < C::PP ? C::NPL * C::A_PLANE + pos * 16 : -1;
+      b_pos[i] = pos < PP ? C::NPL * C::A_PLANE + pos * 16 : -1;
     }
     WS_STAMP_DECL;
     // load cursor: item ld (index v_ld), chunk ch_ld
@@ -900,9 +944,9 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 #pragma unroll
       for (int i = 0; i < B_IT; ++i) {
         const int pos = ptid + i * PT;
-        const int r = pos / C::PW, c = pos % C::PW;
+        const int r = pos / PW, c = pos % PW;
         const int gh = ld.h0 - 1 + r, gw = ld.w0 - 1 + c;
-        b_goff[i] = pos < C::PP && gh >= 0 && gh < H && gw >= 0 && gw < W ? gh * W + gw : -1;
+        b_goff[i] = pos < PP && gh >= 0 && gh < H && gw >= 0 && gw < W ? gh * W + gw : -1;
       }
       x_rsrc = make_buffer_rsrc(X + (size_t)ld.n * Cin * HWi, (unsigned)Cin * HWi * 4u);
     };
@@ -1030,23 +1074,36 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
   const int l16 = lane & 15, g = lane >> 4;
   constexpr int RB = MI * 2, CB = NJ * 2;
   const int a_lane = (wm * MI * 32 + l16) * C::AROW;
-  auto tap_c = [&](int tap) { return ((tap / 3) * C::PW + tap % 3) * 16; };
-  // column block cb sits at a compile-time offset from column block 0
-  const int bp0 = C::NPL * C::A_PLANE + (wn * NJ * C::PW + l16) * 16;
-  auto baddr = [&](int cb, int bo) { return bo + ((cb >> 1) * C::PW + (cb & 1) * 16) * 16; };
+  auto tap_c = [&](int tap) { return ((tap / 3) * PW + tap % 3) * 16; };
+  // column block cb: this lane's pixel q = 64 wn + 16 cb + l16 of the tile, at patch
+  // position (q / TW) * PW + q % TW for tap (0, 0); pixels past the tile read position 0
+  // (their results are never stored)
+  int bpix[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    const int q = wn * 64 + cb * 16 + l16;
+    bpix[cb] = C::NPL * C::A_PLANE + (q < TH * TW ? (q / TW) * PW + q % TW : 0) * 16;
+  }
+  // (the asm keeps the compiler from hoisting all 20 (unit, block) sums out of the loop
+  // into registers)
+  auto baddr = [&](int cb, int bo) {
+    int bp = bpix[cb];
+    asm volatile("" : "+v"(bp));
+    return bo + bp;
+  };
   auto ua = [&](int u) { return (u >= 9 ? C::BUF : 0) + 16 * (u % 9); };
   auto ub = [&](int u) { return (u >= 9 ? C::BUF : 0) + tap_c(u % 9); };
   int aoff[4], boff[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     aoff[s] = a_lane + ua(4 * s + g);
-    boff[s] = bp0 + ub(4 * s + g);
+    boff[s] = ub(4 * s + g);
   }
   const int hb = 8 * (g & 1);
   const int aoff4 = a_lane + ua(16 + (lane >> 5)) + hb;
-  const int boff4 = bp0 + ub(16 + (lane >> 5)) + hb;
+  const int boff4 = ub(16 + (lane >> 5)) + hb;
   // lone last chunk: (8, pad) — slot 9 of a weight row is zero
-  const int aoffL = a_lane + 16 * (8 + (lane >> 5)) + hb, boffL = bp0 + tap_c(8) + hb;
+  const int aoffL = a_lane + 16 * (8 + (lane >> 5)) + hb, boffL = tap_c(8) + hb;
 
   f32x4 acc[RB][CB];
   auto step16 = [&](int ao, int bo) {
@@ -1084,7 +1141,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     }
   };
 
-  constexpr int TP = C::TH * C::TW;
+  constexpr int TP = C::TPIX;
   const bool has_scale = epi.scale != nullptr;
   WS_STAMP_DECL;
   int k = 0;
@@ -1141,7 +1198,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
-            St[ml * TP + (wn * NJ + (cb >> 1)) * C::TW + (cb & 1) * 16 + l16] = acc[rb][cb][r];
+            St[ml * TP + wn * 64 + cb * 16 + l16] = acc[rb][cb][r];
           }
       WS_STAMP(7);
       continue;
@@ -1149,8 +1206,9 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     bool pooled = false;
     if constexpr (NJ == 2) {
       if (epi.pool) {
-        // max_pool2d(2, 2) window: pixel rows j = 0, 1 (column blocks hh and 2 + hh), columns
-        // (l16, l16 ^ 1); torch's window order and update rule, as conv_fwd_bs_kernel
+        // max_pool2d(2, 2) window (16 x 32 tiles only, see ws_tile): pixel rows j = 0, 1
+        // (column blocks hh and 2 + hh), columns (l16, l16 ^ 1); torch's window order and
+        // update rule, as conv_fwd_bs_kernel
         pooled = true;
         const int Hp = H / 2, Wp2 = W / 2;
         float* Pn = epi.pool + (size_t)it.n * Cout * Hp * Wp2;
@@ -1189,8 +1247,9 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
-          const int h = it.h0 + wn * NJ + (cb >> 1), w = it.w0 + (cb & 1) * 16 + l16;
-          if (h >= H || w >= W) continue;
+          const int q = wn * 64 + cb * 16 + l16;
+          const int h = it.h0 + q / TW, w = it.w0 + q % TW;
+          if (q >= TH * TW || h >= H || w >= W) continue;
           const int pix = h * W + w;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1687,11 +1746,13 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
 // y = act(sum_s slab[s] + bias), summed in split order (deterministic).
 // Sum the split-K partial tiles of the tail tiles in fixed split order (deterministic),
 // apply the epilogue and scatter to Y.  One workgroup per (tail tile, 1024 elements).
+// A tile is th_rows x tw_cols pixels (band: tp consecutive flattened pixels), its slab
+// rows tp apart.
 __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
-    const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int th_rows,
-    int tiles_m, int tiles_w, int tiles_h, Epi epi, int Cout, int H, int W,
-    float* __restrict__ Y, int band) {
-  const int tp = th_rows * 32, tile_elems = bm * tp;
+    const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tp,
+    int th_rows, int tw_cols, int tiles_m, int tiles_w, int tiles_h, Epi epi, int Cout, int H,
+    int W, float* __restrict__ Y, int band) {
+  const int tile_elems = bm * tp;
   const int per_tile = (tile_elems + 1023) / 1024;
   const int ti = blockIdx.x / per_tile;
   int t = dp_tiles + ti;
@@ -1710,8 +1771,8 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
       p = tw * tp + pix;
       if (co >= Cout || p >= H * W) continue;
     } else {
-      const int h = th * th_rows + pix / 32, w = tw * 32 + pix % 32;
-      if (co >= Cout || h >= H || w >= W) continue;
+      const int h = th * th_rows + pix / tw_cols, w = tw * tw_cols + pix % tw_cols;
+      if (co >= Cout || pix >= th_rows * tw_cols || h >= H || w >= W) continue;
       p = h * W + w;
     }
     float v = S[e];
@@ -1721,7 +1782,12 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
     if (epi.bias) v += epi.bias[co];
     if (epi.residual) v += epi.residual[idx];
     if (epi.relu) v = fmaxf(v, 0.f);
-    Y[idx] = v;
+    if (epi.s2d > 1) {
+      const long long o = epi_out_index(epi, n, co, p / W, p % W, Cout, H, W);
+      if (o >= 0) Y[o] = v;
+    } else {
+      Y[idx] = v;
+    }
   }
 }
 
@@ -1846,6 +1912,7 @@ struct FwdPlan {
   int cps;       // input-channel chunks per split piece
   int n_tail() const { return tiles_m * tiles_w * tiles_h * n - dp_tiles; }
   int n;
+  int th = 0, tw = 0;  // warp-specialized kernel: tile rows x columns (ws_tile)
   size_t slab_bytes(int bm, int th) const {
     return ksplit > 1 ? (size_t)ksplit * n_tail() * bm * th * 32 * sizeof(float) : 0;
   }
@@ -1939,8 +2006,8 @@ static int launch_fwd(const float* X, const float* Wk, Epi epi, float* Y, int N,
   if (p.ksplit > 1) {
     const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
     hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
-                       p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
-                       p.tiles_h, epi, Cout, H, W, Y, 0);
+                       p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH * C::TW, C::TH, C::TW,
+                       p.tiles_m, p.tiles_w, p.tiles_h, epi, Cout, H, W, Y, 0);
     TLOD_LAUNCH_CHECK();
   }
   return kOk;
@@ -2005,6 +2072,33 @@ static bool use_ws(int Cin, int H, int W) {
   return ws && Cin >= 128 && (TLOD_WS_FLAT != 0 || (size_t)Cin * H * W * 4 < (1ull << 31));
 }
 
+// Tile of the warp-specialized kernel for an H x W map: the fewest tiles of TH x TW <= 512
+// pixels whose (TH + 2) x (TW + 2) patch fits kWsPos positions; ties go to the smaller halo
+// (patch / pixels, to 0.05), then the wider tile (coalesced staging rows).  Pooling epilogues
+// and TLOD_WS_FLEX=0 keep 16 x 32.
+struct WsTile {
+  int th, tw;
+};
+static WsTile ws_tile(int H, int W, bool pool) {
+  static const bool flex = tune_knob("TLOD_WS_FLEX", 1) != 0;
+  if (pool || !flex) return {16, 32};
+  WsTile best{16, 32};
+  long long best_t = (long long)div_up(H, 16) * div_up(W, 32);
+  int best_h = 24;  // halo of 16 x 32 (612 / 512 = 1.195) in units of 0.05
+  for (int th = 1; th <= std::min(H, 64); ++th) {
+    const int tw = std::min({512 / th, kWsPos / (th + 2) - 2, W});
+    if (tw < 8) continue;
+    const long long t = (long long)div_up(H, th) * div_up(W, tw);
+    const int halo = (int)std::lround(20.0 * (th + 2) * (tw + 2) / (th * tw));
+    if (t < best_t || (t == best_t && (halo < best_h || (halo == best_h && tw > best.tw)))) {
+      best = {th, tw};
+      best_t = t;
+      best_h = halo;
+    }
+  }
+  return best;
+}
+
 template <int WM, int WN, int MI, int NJ, int NP>
 static int ws_slots() {
   static const int slots = resident_slots(conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP, true>,
@@ -2019,15 +2113,26 @@ static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_sp
   static const int slots_plain = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>,
                                                 C::NT, C::LDS_BYTES);
   int slots = slots_plain;
+  WsTile wt{C::TH, C::TW};
+  bool ws = false;
   if constexpr (!BAND)
-    if (use_ws(Cin, H, W)) slots = ws_slots<WM, WN, MI, NJ, NP>();
+    if (use_ws(Cin, H, W)) {
+      ws = true;
+      slots = ws_slots<WM, WN, MI, NJ, NP>();
+      wt = ws_tile(H, W, !allow_split);  // allow_split == false: the pooling epilogue
+    }
   const int nchunks = div_up(Cin, C::CK);
   // cost model in f32-MFMA-equivalent time: the split products run ~16/NP x faster
-  const int tw = BAND ? div_up(H * W, C::TH * C::TW) : div_up(W, C::TW);
-  const int th = BAND ? 1 : div_up(H, C::TH);
-  return plan_schedule(div_up(Cout, C::BM), tw, th, N, nchunks,
-                       2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
-                       C::BM * C::TH * C::TW, slots, allow_split);
+  const int tw = BAND ? div_up(H * W, C::TH * C::TW) : div_up(W, wt.tw);
+  const int th = BAND ? 1 : div_up(H, wt.th);
+  FwdPlan p = plan_schedule(div_up(Cout, C::BM), tw, th, N, nchunks,
+                            2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
+                            C::BM * C::TH * C::TW, slots, allow_split);
+  if (ws) {
+    p.th = wt.th;
+    p.tw = wt.tw;
+  }
+  return p;
 }
 
 template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
@@ -2061,7 +2166,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
       const long long grid = persist ? std::min<long long>(nwg, ws_slots<WM, WN, MI, NJ, NP>()) : nwg;
       hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C::NT + kProdWaves * 64), WC::LDS_BYTES,
                          s, X, Wp, epi, Y, N, Cin, H, W, Cout, p.tiles_m, p.tiles_w, p.tiles_h,
-                         p.dp_tiles, p.ksplit, p.cps, slab);
+                         p.dp_tiles, p.ksplit, p.cps, slab, p.th, p.tw);
       launched = true;
     }
   }
@@ -2079,9 +2184,10 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
   TLOD_LAUNCH_CHECK();
   if (p.ksplit > 1) {
     const int per_tile = div_up(C::BM * C::TH * C::TW, 1024);
+    const int th = p.th ? p.th : C::TH, tw = p.th ? p.tw : C::TW;
     hipLaunchKernelGGL(fwd_tail_reduce_kernel, dim3(p.n_tail() * per_tile), dim3(256), 0, s, slab,
-                       p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH, p.tiles_m, p.tiles_w,
-                       p.tiles_h, epi, Cout, H, W, Y, BAND ? 1 : 0);
+                       p.ksplit, p.n_tail(), p.dp_tiles, C::BM, C::TH * C::TW, th, tw, p.tiles_m,
+                       p.tiles_w, p.tiles_h, epi, Cout, H, W, Y, BAND ? 1 : 0);
     TLOD_LAUNCH_CHECK();
   }
   return kOk;
@@ -2109,7 +2215,9 @@ static int conv_fwd_bs_dispatch(const float* X, const unsigned short* Wp, Epi ep
     return launch_fwd_bs<WM_, WN_, MI_, NJ_, NP_, BAND_>(X, Wp, epi, Y, N, Cin, H, W, Cout,     \
                                                          slab, sb, s);                          \
   } while (0)
-  const bool band = use_band(H, W) && epi.pool == nullptr;  // pooling: 2D tiles
+  // pooling: 2D tiles; the warp-specialized kernel's flexible tiles replace band tiles
+  const bool band = use_band(H, W) && epi.pool == nullptr &&
+                    !(use_ws(Cin, H, W) && tune_knob("TLOD_WS_FLEX", 1) != 0);
   if (nprod == 6 && band) TLOD_BS_CFG(1, 8, 2, 2, 6, true);
   if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6, false);
   if (band) TLOD_BS_CFG(1, 8, 2, 2, 3, true);
@@ -2302,6 +2410,17 @@ extern "C" int tlod_conv_fwd_ex_f32(const float* x, const float* wk, const float
   TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
   return conv_fwd_dispatch(x, wk, Epi{scale, bias, residual, relu}, y, N, Cin, H, W, Cout, KS,
                            (float*)ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int tlod_drm_fwd_f32(const float* x, const float* wk, float* y, int N, int Cin,
+                                int H, int W, int Cout, int scale, void* ws, size_t ws_bytes,
+                                tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && Cout > 0 && scale > 1 && H >= scale && W >= scale,
+                 "bad shape (need scale > 1, H, W >= scale)");
+  Epi e{nullptr, nullptr, nullptr, 1};
+  e.s2d = scale;
+  return conv_fwd_dispatch(x, wk, e, y, N, Cin, H, W, Cout, 1, (float*)ws, ws_bytes,
+                           (hipStream_t)stream);
 }
 
 extern "C" int tlod_conv_dgrad_f32(const float* dy, const float* wd, float* dx, int N, int Cin,

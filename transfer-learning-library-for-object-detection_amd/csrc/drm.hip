@@ -27,7 +27,10 @@ __global__ void __launch_bounds__(256) s2d_kernel(const float* __restrict__ x, i
   }
 }
 
-__global__ void __launch_bounds__(256) d2s_kernel(const float* __restrict__ dy, int C, int H,
+// dx = depth_to_space(dy) (cropped positions 0); with y (the forward's ReLU output in the
+// space-to-depth layout) also the ReLU backward: dx = depth_to_space(dy * (y > 0)).
+__global__ void __launch_bounds__(256) d2s_kernel(const float* __restrict__ dy,
+                                                  const float* __restrict__ y, int C, int H,
                                                   int W, int s, int Ho, int Wo, size_t total,
                                                   float* __restrict__ dx) {
   const int ss = s * s;
@@ -43,7 +46,9 @@ __global__ void __launch_bounds__(256) d2s_kernel(const float* __restrict__ dy, 
     float v = 0.f;
     if (h < Ho && w < Wo) {
       const int cc = c * ss + (xh % s) * s + (xw % s);
-      v = dy[((b * C * ss + cc) * Ho + h) * Wo + w];
+      const size_t i = ((b * C * ss + cc) * Ho + h) * Wo + w;
+      v = dy[i];
+      if (y && !(y[i] > 0.f)) v = 0.f;
     }
     dx[o] = v;
   }
@@ -75,8 +80,23 @@ extern "C" int tlod_depth_to_space_f32(const float* dy, int B, int C, int H, int
                  "bad shape (need H, W >= scale)");
   const int Ho = H / scale, Wo = W / scale;
   const size_t total = (size_t)B * C * H * W;
-  hipLaunchKernelGGL(d2s_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dy, C,
-                     H, W, scale, Ho, Wo, total, dx);
+  hipLaunchKernelGGL(d2s_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dy,
+                     nullptr, C, H, W, scale, Ho, Wo, total, dx);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+// Backward of the fused DRM forward (tlod_drm_fwd_f32: 1x1 conv + ReLU + crop +
+// space-to-depth, lib/MAF/drm.py:10-42) up to the conv: g = depth_to_space(dy * (y > 0)),
+// one pass (the reference runs the cat/reshape/chunk backward and the ReLU backward apart).
+extern "C" int tlod_drm_relu_bwd_f32(const float* dy, const float* y, int B, int C, int H, int W,
+                                     int scale, float* g, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && scale > 1 && H >= scale && W >= scale && dy && y && g,
+                 "bad shape (need scale > 1, H, W >= scale)");
+  const int Ho = H / scale, Wo = W / scale;
+  const size_t total = (size_t)B * C * H * W;
+  hipLaunchKernelGGL(d2s_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dy, y,
+                     C, H, W, scale, Ho, Wo, total, g);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

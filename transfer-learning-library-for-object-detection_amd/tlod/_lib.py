@@ -118,6 +118,9 @@ SIGNATURES = {
                                 c_float, c_float, P, P, P, P]),
     "tlod_space_to_depth_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_depth_to_space_f32": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_drm_fwd_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_size_t,
+                                 P]),
+    "tlod_drm_relu_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "tlod_relu_dropout_f32": (c_int, [P, P, ctypes.c_longlong, c_float, c_uint64, P]),
     "tlod_relu_dropout_bwd_f32": (c_int, [P, P, P, ctypes.c_longlong, c_float, P]),
     "tlod_rpn_loss_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, P, P,

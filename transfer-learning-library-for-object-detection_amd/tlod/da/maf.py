@@ -56,8 +56,55 @@ def space_to_depth(x, scale):
     return SpaceToDepthFunction.apply(x, scale)
 
 
+class DRMFunction(torch.autograd.Function):
+    """The whole DRM (drm.py:10-42: conv_low_dim 1x1 without bias -> ReLU -> crop ->
+    space-to-depth) as one conv launch whose epilogue stores every output at its
+    space-to-depth position (tlod_drm_fwd_f32; the (B, C, H, W) map is never written), and
+    its backward as one depth-to-space + ReLU-mask pass (tlod_drm_relu_bwd_f32) ahead of the
+    1x1 dgrad / wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, weight, scale, tap=None):
+        from ..conv import _check, pack_fwd
+        _check(x, weight)
+        x = x.contiguous()
+        B, Cin, H, W = x.shape
+        C, s = weight.shape[0], int(scale)
+        L = _lib.lib()
+        y = torch.empty((B, C * s * s, H // s, W // s), dtype=x.dtype, device=x.device)
+        ws = _lib.workspace(L.tlod_conv_fwd_workspace_bytes(B, Cin, H, W, C, 1), x.device, "conv")
+        _lib.check(L.tlod_drm_fwd_f32(_lib.ptr(x), _lib.ptr(pack_fwd(weight)), _lib.ptr(y), B, Cin,
+                                      H, W, C, s, _lib.ptr(ws), ws.numel(), _lib.stream_of(x)),
+                   "drm_fwd")
+        if tap is not None:  # test instrumentation: the ReLU map (0 on the cropped border)
+            m = torch.empty((B, C, H, W), dtype=y.dtype, device=y.device)
+            _lib.check(L.tlod_depth_to_space_f32(_lib.ptr(y), B, C, H, W, s, _lib.ptr(m),
+                                                 _lib.stream_of(y)), "depth_to_space")
+            tap.append(m)
+        ctx.meta = (B, C, H, W, s)
+        ctx.wparam = weight
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..conv import conv_dgrad, conv_wgrad
+        from ..grads import grad_out
+        x, weight, y = ctx.saved_tensors
+        B, C, H, W, s = ctx.meta
+        dy = dy.contiguous()
+        g = torch.empty((B, C, H, W), dtype=dy.dtype, device=dy.device)
+        _lib.check(_lib.lib().tlod_drm_relu_bwd_f32(_lib.ptr(dy), _lib.ptr(y), B, C, H, W, s,
+                                                    _lib.ptr(g), _lib.stream_of(dy)),
+                   "drm_relu_bwd")
+        dx = conv_dgrad(g, weight) if ctx.needs_input_grad[0] else None
+        dw = conv_wgrad(g, x, 1, out=grad_out(ctx.wparam)) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None
+
+
 class DRM(nn.Module):
-    """lib/MAF/drm.py:10-42 (conv_low_dim 1x1 no bias, ReLU fused into its epilogue)."""
+    """lib/MAF/drm.py:10-42; conv_low_dim (1x1, no bias) keeps the reference's module and
+    state_dict key, its ReLU, crop and space-to-depth run fused (DRMFunction)."""
 
     def __init__(self, in_dim, inner_channel, scale):
         super().__init__()
@@ -65,7 +112,8 @@ class DRM(nn.Module):
         self.conv_low_dim = Conv2d(in_dim, inner_channel, 1, bias=False, relu=True)
 
     def forward(self, x):
-        return space_to_depth(self.conv_low_dim(x), self.scale)
+        return DRMFunction.apply(x, self.conv_low_dim.weight, self.scale,
+                                 self.conv_low_dim.act_tap)
 
 
 class WGRLayer(torch.autograd.Function):
