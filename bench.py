@@ -244,6 +244,9 @@ def main():
         "conv_math": {"3x3 fwd/dgrad": tconv.conv_math(), "3x3 and 1x1 wgrad": tconv.wgrad_math(),
                       "1x1 fwd/dgrad": "f32", "fc6/fc7/DA fc": linear_math()},
         "mean_loss": round(last_loss, 4),
+        # ReLU backward passes folded into the next conv's dgrad epilogue, per step (tlod.conv)
+        "fused_relu_backward_per_step": {k: v / (a.steps + a.warmup)
+                                         for k, v in tconv.STATS.items()},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and a.cpu_baseline_steps > 0 and a.method == "daf" \

@@ -71,9 +71,14 @@ int tlod_roi_align_bwd_f32(const float* top_grad, int B, int C, int H, int W,
 int tlod_roi_align_avg_fwd_f32(const float* feat, int B, int C, int H, int W,
                                const float* rois, int R, int ph, int pw, float scale,
                                float* out, tlod_stream_t stream);
-/* avg backward: with a workspace (tlod_roi_align_avg_bwd_workspace_bytes) the atomics go
- * to a (B,H,W,C) accumulator (lanes over channels: contiguous atomics) that is then added
- * into bottom_grad; ws == NULL accumulates straight into NCHW. */
+/* avg backward, ADDED into bottom_grad (roi_align_kernel.cu:94-143 + avg_pool2d's backward).
+ * With ws_bytes >= tlod_roi_align_avg_bwd_gather_workspace_bytes: no atomics — the taps are
+ * sorted by feature cell and every (cell, channel) gathers its contributions in a fixed
+ * order (deterministic; ~R*64*(C+16)*4 B of workspace).  Otherwise, with ws_bytes >=
+ * tlod_roi_align_avg_bwd_workspace_bytes: float atomics into a (B,H,W,C) accumulator then
+ * added into bottom_grad; ws == NULL: atomics straight into NCHW. */
+size_t tlod_roi_align_avg_bwd_gather_workspace_bytes(int B, int C, int H, int W, int R, int ph,
+                                                     int pw);
 size_t tlod_roi_align_avg_bwd_workspace_bytes(int B, int C, int H, int W);
 int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W,
                                const float* rois, int R, int ph, int pw, float scale,
@@ -255,12 +260,28 @@ int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float* scale, con
                          tlod_stream_t stream);
 /* Split-bf16 wgrad: tlod_conv_wgrad_f32's result (same argument meaning, same
  * deterministic split-K slab reduction) with dy and x split into bf16 planes on the fly and
- * nprod (6 or 3) products on the bf16 MFMA.  No weight pack.  KS = 1 or 3. */
+ * nprod (6 or 3) products on the bf16 MFMA.  No weight pack.  KS = 1 or 3.  db (optional,
+ * Cout floats): the bias gradient sum_{n,h,w} dy, from the staged dy rows in the same
+ * launch (replaces the bias-gradient half of the ReLU backward pass). */
 size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
                                           int nprod);
-int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, int accumulate, int N,
-                           int Cin, int H, int W, int Cout, int KS, int nprod, void* ws,
+int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, float* db, int accumulate,
+                           int N, int Cin, int H, int W, int Cout, int KS, int nprod, void* ws,
                            size_t ws_bytes, tlod_stream_t stream);
+/* Direct 3x3 conv (stride 1, pad 1) for Cin <= 4 — VGG16 conv1_1 on the image
+ * (lib/DAF/vgg16.py:49 features[0]): y = act(conv(x, weight) + bias), weight the nn.Conv2d
+ * (Cout, Cin, 3, 3) tensor as is, exact f32 FMA chains (27 per output for Cin = 3). */
+int tlod_conv3x3_direct_f32(const float* x, const float* weight, const float* bias, float* y,
+                            int N, int Cin, int H, int W, int Cout, int relu,
+                            tlod_stream_t stream);
+/* Split-bf16 3x3 dgrad with the previous layer's ReLU backward in the epilogue:
+ * dx = tlod_conv_fwd_bs_f32(dy, P_dgrad, ...) * (mask > 0), mask (N, Cin, H, W) = the
+ * previous conv's ReLU output (this conv's input, lib/DAF/vgg16.py:49 features).  Cin / Cout
+ * as in tlod_conv_fwd_bs_f32's dgrad form (Cin := the layer's Cout, Cout := the layer's Cin);
+ * workspace: tlod_conv_fwd_bs_workspace_bytes of that form. */
+int tlod_conv_dgrad_bs_mask_f32(const float* dy, const void* wp, const float* mask, float* dx,
+                                int N, int Cin, int H, int W, int Cout, int nprod, void* ws,
+                                size_t ws_bytes, tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ Split-bf16 GEMM
  * Replaces: the cuBLAS fp32 GEMMs of nn.Linear in RCNN_top (fc6/fc7, lib/DAF/vgg16.py:67-71
@@ -285,6 +306,20 @@ int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c
 size_t tlod_conv3x3_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
                                             int w_layout, int nprod);
 int tlod_conv3x3_gemm_bs_f32(const float* x, const float* w, int w_layout, const float* scale,
+                             const float* bias, const float* residual, float* y, int N, int Cin,
+                             int H, int W, int Cout, int relu, int nprod, void* ws,
+                             size_t ws_bytes, tlod_stream_t stream);
+/* The same for 1x1 convolutions (replaces the cuDNN 1x1 convs of the ResNet101 bottlenecks,
+ * lib/DAF/resnet.py:64-102 — conv1 / conv3 / downsample, with the frozen BatchNorm folded into
+ * scale / bias and the residual add + ReLU of conv3 in the epilogue — and the DA heads'
+ * 1x1 convs, lib/DAF/DA.py:19-33): per image y = W (Cout x Cin) . x (Cin x H*W).  w_layout =
+ * 0: w is the nn.Conv2d weight (Cout, Cin, 1, 1) (forward); 1: the input gradient, x = dy,
+ * w the same (layer Cout, layer Cin) weight read transposed, Cin := the layer's Cout,
+ * Cout := the layer's Cin.  Output-channel tiles of 64 / 128 / 256 rows, whichever fills the
+ * chip best (conv1x1_mi). */
+size_t tlod_conv1x1_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
+                                            int w_layout, int nprod);
+int tlod_conv1x1_gemm_bs_f32(const float* x, const float* w, int w_layout, const float* scale,
                              const float* bias, const float* residual, float* y, int N, int Cin,
                              int H, int W, int Cout, int relu, int nprod, void* ws,
                              size_t ws_bytes, tlod_stream_t stream);

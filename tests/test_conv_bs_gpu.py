@@ -110,12 +110,62 @@ def test_conv_bs_wgrad(math, N, Cin, Cout, H, W):
     x = torch.randn(N, Cin, H, W, generator=g)
     gy = torch.randn(N, Cout, H, W, generator=g)
     ref = torch.nn.grad.conv2d_weight(x.double(), (Cout, Cin, 3, 3), gy.double(), padding=1)
-    dw = conv_wgrad(gy.to(dev), x.to(dev), 3, math=math)
+    db = torch.empty(Cout, device=dev)
+    dw = conv_wgrad(gy.to(dev), x.to(dev), 3, math=math, db=db)
     _close(dw, ref, math)
+    # the bias gradient from the same launch (row sums of the staged dy), f32 summation
+    _close(db, gy.double().sum((0, 2, 3)), "bf16x6")
     base = torch.randn(Cout, Cin, 3, 3, generator=g)
     acc = base.to(dev).clone()
     conv_wgrad(gy.to(dev), x.to(dev), 3, out=acc, accumulate=True, math=math)
     _close(acc, ref + base.double(), math)
+
+
+def test_masked_dgrad_is_dgrad_times_mask():
+    """tlod_conv_dgrad_bs_mask_f32 = the dgrad with the previous layer's ReLU backward in the
+    epilogue: bit-identical to conv_dgrad(...) * (mask > 0), including the split-K tail tiles
+    (conv5-shaped map) and the plain-kernel shapes (Cin < 128)."""
+    from tlod.conv import conv_dgrad
+    g = torch.Generator().manual_seed(3)
+    for N, Cin, Cout, H, W in [(2, 512, 512, 37, 75), (1, 64, 128, 40, 57), (2, 256, 256, 75, 150)]:
+        gy = torch.randn(N, Cout, H, W, generator=g).to(dev)
+        w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.05).to(dev)
+        m = torch.relu(torch.randn(N, Cin, H, W, generator=g)).to(dev)
+        a = conv_dgrad(gy, w, math="bf16x6", mask=m)
+        b = conv_dgrad(gy, w, math="bf16x6") * (m > 0)
+        assert torch.equal(a, b)
+
+
+def test_fused_relu_backward_chain(monkeypatch):
+    """A conv -> conv -> conv chain of fused-ReLU convs: the inner ReLU backward passes run in
+    the next conv's dgrad epilogue and the bias gradients come from the wgrad launches
+    (STATS counters), with the same gradients as the unfused backward (input gradients
+    bit-identical, bias gradients to f32 summation order)."""
+    import tlod.conv as tc
+    g = torch.Generator().manual_seed(9)
+    mods = [tc.Conv2d(c_in, c_out, 3, relu=True).to(dev)
+            for c_in, c_out in [(64, 128), (128, 128), (128, 256)]]
+    x0 = torch.randn(2, 64, 30, 47, generator=g).to(dev)
+    gy = torch.randn(2, 256, 30, 47, generator=g).to(dev)
+
+    def run():
+        for m in mods:
+            m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = x
+        for m in mods:
+            y = m(y)
+        y.backward(gy)
+        return [x.grad] + [t.grad.clone() for m in mods for t in (m.weight, m.bias)]
+    before = dict(tc.STATS)
+    fused = run()
+    assert tc.STATS["masked_dgrad"] - before["masked_dgrad"] == 2
+    assert tc.STATS["relu_bwd_skipped"] - before["relu_bwd_skipped"] == 2
+    monkeypatch.setattr(tc, "_relu_out", lambda x: False)
+    plain = run()
+    assert torch.equal(fused[0], plain[0])
+    for a, b in zip(fused[1:], plain[1:]):
+        _close(a, b.double(), "bf16x6")
 
 
 def test_conv_bs_wgrad_deterministic_and_f32_accurate():
@@ -150,6 +200,37 @@ def test_conv_bs_epilogue(math):
     ref = F.relu(F.conv2d(x.double(), w.double(), padding=1) * sc.double().view(1, -1, 1, 1)
                  + sh.double().view(1, -1, 1, 1) + r.double())
     _close(y, ref, math)
+
+
+ONE_SHAPES = [  # N, Cin, Cout, H, W: ResNet101 bottleneck 1x1s (layer2 / layer3 at 600x1200),
+    # the 64-, 128- and 256-row tiles, ragged channel / pixel counts
+    (2, 1024, 256, 38, 75), (2, 256, 1024, 38, 75), (2, 512, 128, 75, 150), (1, 64, 64, 30, 41),
+    (3, 96, 80, 9, 33), (1, 72, 257, 5, 7), (2, 130, 200, 1, 3),
+]
+
+
+@pytest.mark.parametrize("math", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("N,Cin,Cout,H,W", ONE_SHAPES)
+def test_conv1x1_gemm_fwd_dgrad(math, N, Cin, Cout, H, W):
+    """1x1 forward (folded-BN scale / shift + residual + ReLU epilogue) and input gradient on
+    the split-bf16 conv GEMM (tlod_conv1x1_gemm_bs_f32) vs fp64."""
+    from tlod.conv import _gemm1x1, conv_dgrad, conv_fwd
+    assert _gemm1x1(1, math, Cin, Cout)
+    g = torch.Generator().manual_seed(N * 7 + Cin + Cout + H)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) * (2.0 / Cin) ** 0.5
+    sc, sh = torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g)
+    r = torch.randn(N, Cout, H, W, generator=g)
+    y = conv_fwd(x.to(dev), w.to(dev), sh.to(dev), relu=True, scale=sc.to(dev), residual=r.to(dev),
+                 math=math)
+    ref = F.relu(F.conv2d(x.double(), w.double()) * sc.double().view(1, -1, 1, 1)
+                 + sh.double().view(1, -1, 1, 1) + r.double())
+    _close(y, ref, math)
+    y0 = conv_fwd(x.to(dev), w.to(dev), None, relu=False, math=math)
+    _close(y0, F.conv2d(x.double(), w.double()), math)
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    dx = conv_dgrad(gy.to(dev), w.to(dev), math=math)
+    _close(dx, torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double()), math)
 
 
 def test_conv_bs_matches_f32_path_closely():
@@ -215,3 +296,51 @@ def test_split_bf16_huge_finite_operands():
     c = gemm(A.to(dev), B.to(dev), 40, 24, 64, 1, 1, None, "bf16x6")
     assert torch.isfinite(c).all()
     _close(c, A.double() @ B.double().t(), "bf16x6")
+
+
+def test_fused_relu_backward_multi_consumer(monkeypatch):
+    """A fused-ReLU conv output read by two consumers (the next conv and a side branch): the
+    next conv's masked dgrad is summed with the branch's gradient by autograd (possibly in
+    place into the tagged tensor), so the ReLU backward must NOT be skipped; the gradients
+    equal the unfused backward's."""
+    import tlod.conv as tc
+    g = torch.Generator().manual_seed(12)
+    c1, c2 = tc.Conv2d(32, 64, 3, relu=True).to(dev), tc.Conv2d(64, 64, 3, relu=True).to(dev)
+    x0 = torch.randn(1, 32, 20, 28, generator=g).to(dev)
+    gy = torch.randn(1, 64, 20, 28, generator=g).to(dev)
+    side = torch.randn(1, 64, 20, 28, generator=g).to(dev)
+
+    def run():
+        for m in (c1, c2):
+            m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y1 = c1(x)
+        loss = (c2(y1) * gy).sum() + (y1 * side).sum()
+        loss.backward()
+        return [x.grad, c1.weight.grad.clone(), c1.bias.grad.clone(), c2.weight.grad.clone()]
+    before = dict(tc.STATS)
+    fused = run()
+    assert tc.STATS["masked_dgrad"] - before["masked_dgrad"] == 1
+    assert tc.STATS["relu_bwd_skipped"] == before["relu_bwd_skipped"]
+    monkeypatch.setattr(tc, "_relu_out", lambda x: False)
+    plain = run()
+    for a, b in zip(fused, plain):
+        _close(a, b.double(), "bf16x6")
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 3, 64, 600, 1200), (1, 3, 64, 37, 300), (1, 1, 7, 5, 260),
+                                           (3, 4, 20, 9, 8)])
+def test_conv3x3_direct(N, Cin, Cout, H, W):
+    """Direct f32 3x3 conv for Cin <= 4 (VGG16 conv1_1 on the image, fused bias + ReLU) vs
+    fp64: f32 FMA chains, 1e-6 normwise."""
+    from tlod.conv import conv_fwd
+    g = torch.Generator().manual_seed(Cin * 100 + Cout + W)
+    x = torch.randn(N, Cin, H, W, generator=g) * 50
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * 0.2
+    b = torch.randn(Cout, generator=g)
+    for relu in (True, False):
+        y = conv_fwd(x.to(dev), w.to(dev), b.to(dev), relu=relu)
+        ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+        ref = F.relu(ref) if relu else ref
+        got = y.double().cpu()
+        assert float((got - ref).norm() / ref.norm()) < 1e-6

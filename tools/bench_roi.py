@@ -1,6 +1,7 @@
 """Microbenchmark: RoIAlignAvg 7x7 backward on the DAF step's shape (2 images, base feature
-512 x 37 x 75, 256 source + 300 target RoIs of realistic sizes).  TLOD_ROI_BWD_LDS=0 selects
-the global-atomic kernels."""
+512 x 37 x 75, 256 source + 300 target RoIs of realistic sizes): the default gather
+backward: the global-atomic NHWC kernel (default), TLOD_ROI_BWD_GATHER=1 the gather kernel
+(sorted taps, no atomics), TLOD_ROI_BWD_LDS=1 the LDS-accumulation kernel."""
 import json
 import os
 import sys
@@ -30,7 +31,9 @@ def main():
     top = torch.randn(R, C, 7, 7, device=dev)
     grad = torch.zeros(B, C, H, W, device=dev)
     L = _lib.lib()
-    ws = torch.empty(L.tlod_roi_align_avg_bwd_workspace_bytes(B, C, H, W), dtype=torch.uint8, device=dev)
+    wsb = max(L.tlod_roi_align_avg_bwd_gather_workspace_bytes(B, C, H, W, R, 7, 7),
+              L.tlod_roi_align_avg_bwd_workspace_bytes(B, C, H, W))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
     def run():
         _lib.check(L.tlod_roi_align_avg_bwd_f32(_lib.ptr(top), B, C, H, W, _lib.ptr(r), R, 7, 7,
@@ -46,7 +49,9 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / 20 * 1e3
-    print(json.dumps({"lds": os.environ.get("TLOD_ROI_BWD_LDS", "1"), "roi_align_avg_bwd_us": round(us, 1),
+    kind = ("gather" if os.environ.get("TLOD_ROI_BWD_GATHER") == "1" else
+            "lds" if os.environ.get("TLOD_ROI_BWD_LDS") == "1" else "atomic")
+    print(json.dumps({"kernel": kind, "roi_align_avg_bwd_us": round(us, 1),
                       "R": R, "C": C, "map": [H, W]}))
 
 

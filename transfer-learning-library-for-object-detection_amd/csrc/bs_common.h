@@ -18,6 +18,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Exact split x = hi + mid + lo into bf16 terms: hi = the truncated top 8 significant bits
 // (exact and finite for every finite x), mid and lo the round-to-nearest-even bf16 of the

@@ -84,7 +84,14 @@ struct Epi {
   int s2d;      // conv_fwd_kernel only (MAF DRM, lib/MAF/drm.py:20-42): > 1 stores the result
                 // cropped to (H/s*s, W/s*s) and space-to-depth rearranged, (N, Cout*s*s, H/s,
                 // W/s) with channel co*s*s + (h%s)*s + w%s; no residual
+  const float* mask;  // dgrad of a conv whose input is the previous conv's ReLU output: the
+                      // result is zeroed where mask (that input, same layout as y) is not > 0
+                      // — the previous layer's ReLU backward, applied in this epilogue
 };
+
+__device__ __forceinline__ float epi_mask(const Epi& e, size_t idx, float v) {
+  return e.mask && !(e.mask[idx] > 0.f) ? 0.f : v;
+}
 
 // Element offset of output (n, co, h, w) under the epilogue's store layout; -1: cropped by
 // the DRM space-to-depth.
@@ -352,6 +359,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
           v += bias_s[ml];
           if (Rn) v += Rn[idx];
           if (epi.relu) v = fmaxf(v, 0.f);
+          v = epi_mask(epi, (size_t)n * Cout * H * W + idx, v);
           if (epi.s2d > 1) {
             const long long o = epi_out_index(epi, n, co, h, w, Cout, H, W);
             if (o >= 0) Y[o] = v;
@@ -701,7 +709,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
           v += bias_s[ml];
           if (Rn) v += Rn[idx];
           if (epi.relu) v = fmaxf(v, 0.f);
-          Yn[idx] = v;
+          Yn[idx] = epi_mask(epi, (size_t)n * Cout * HWi + idx, v);
         }
       }
     }
@@ -799,9 +807,7 @@ struct WsCfg : BsCfg<WM, WN, MI, NJ, NP, false> {
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x4 mfma16_bf16(u32x4 a, u32x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -1243,29 +1249,62 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     if (!pooled) {
       float* Yn = Y + (size_t)it.n * Cout * HWi;
       const float* Rn = epi.residual ? epi.residual + (size_t)it.n * Cout * HWi : nullptr;
+      const float* Mn = epi.mask ? epi.mask + (size_t)it.n * Cout * HWi : nullptr;
+      int pix[CB];  // -1: outside the tile / map
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
+      for (int cb = 0; cb < CB; ++cb) {
+        const int q = wn * 64 + cb * 16 + l16;
+        const int h = it.h0 + q / TW, w = it.w0 + q % TW;
+        pix[cb] = q < TH * TW && h < H && w < W ? h * W + w : -1;
+      }
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        // residual / mask operands of this row block loaded together, ahead of its stores
+        // (interleaved with the stores they would each pay a full load latency: the
+        // compiler cannot move a load above a store that may alias it)
+        float ext[CB][4];
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
+            const size_t idx = (size_t)co * HWi + pix[cb];
+            const bool ok = pix[cb] >= 0 && co < Cout;
+            ext[cb][r] = Rn ? (ok ? Rn[idx] : 0.f) : Mn ? (ok ? Mn[idx] : 0.f) : 0.f;
+          }
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
-          const int q = wn * 64 + cb * 16 + l16;
-          const int h = it.h0 + q / TW, w = it.w0 + q % TW;
-          if (q >= TH * TW || h >= H || w >= W) continue;
-          const int pix = h * W + w;
+          if (pix[cb] < 0) continue;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
             const int co = it.m0 + ml;
             if (co < Cout) {
-              const size_t idx = (size_t)co * HWi + pix;
+              const size_t idx = (size_t)co * HWi + pix[cb];
               float val = acc[rb][cb][r];
               if (has_scale) val *= scale_s[ml];
               val += bias_s[ml];
-              if (Rn) val += Rn[idx];
+              if (Rn) val += ext[cb][r];
               if (epi.relu) val = fmaxf(val, 0.f);
+              if (Mn && !Rn && !(ext[cb][r] > 0.f)) val = 0.f;
               Yn[idx] = val;
             }
           }
         }
+      }
+      if (Rn && Mn) {  // both (not produced by the library's callers): mask in a second pass
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
+              if (pix[cb] < 0 || co >= Cout) continue;
+              const size_t idx = (size_t)co * HWi + pix[cb];
+              if (!(Mn[idx] > 0.f)) Yn[idx] = 0.f;
+            }
+      }
     }
     WS_STAMP(7);
   }
@@ -1545,11 +1584,14 @@ __device__ __forceinline__ int wg_slot(int row, int px) {
   return TLOD_WG_SWZ ? (((px >> 3) ^ ((row >> 3) & 1)) << 4) + ((px & 4) << 1) : 2 * px;
 }
 
+// db_slab != nullptr: the bias gradient rides along — the workgroups of column tile 0 also
+// sum their staged (masked) dY rows per split, db_slab[split][co] (reduced in split order by
+// db_reduce_kernel): the conv's db = sum_p dY[co][p] without a pass of its own over dY.
 template <int WM, int WN, int MI, int NJ, int KS, int NP>
 __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kernel(
     const float* __restrict__ G, const float* __restrict__ X, float* __restrict__ slab, int N,
     int Cin, int H, int W, int Cout, int tiles_m, int tiles_n, int splits, int chunks_per_split,
-    float inv_w) {
+    float inv_w, float* __restrict__ db_slab) {
   using C = WgBsCfg<WM, WN, MI, NJ, NP>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int KK = KS * KS;
@@ -1664,9 +1706,21 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
     for (int pl = 0; pl < C::NPL; ++pl)
       *reinterpret_cast<uint2*>(dst + pl * plane_bytes) = make_uint2(sp[pl][0], sp[pl][1]);
   };
+  const bool row_sums = db_slab != nullptr && nt == 0;
+  float rs[C::A_IT];  // this lane's 4-pixel segment sums of its dY rows (row_sums)
+#pragma unroll
+  for (int i = 0; i < C::A_IT; ++i) rs[i] = 0.f;
   auto store_chunk = [&](unsigned char* buf) {
 #pragma unroll
-    for (int i = 0; i < C::A_IT; ++i) store_seg(buf + a_lds[i], C::A_PLANE, ra[i], a_mask);
+    for (int i = 0; i < C::A_IT; ++i) {
+      store_seg(buf + a_lds[i], C::A_PLANE, ra[i], a_mask);
+      if (row_sums) {
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += ((a_mask >> e) & 1) ? ra[i][e] : 0.f;
+        rs[i] += t;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) store_seg(buf + b_lds[i], C::B_PLANE, rb[i], b_mask[i]);
   };
@@ -1713,6 +1767,15 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
     __syncthreads();
   }
 
+  if (row_sums) {  // the 4 lanes of a row (tid & 3 = segment), in a fixed order
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      float t = rs[i] + __shfl_xor(rs[i], 1);
+      t = t + __shfl_xor(t, 2);
+      const int row = (tid >> 2) + i * C::ROWS_PER_IT;
+      if ((tid & 3) == 0 && m0 + row < Cout) db_slab[(size_t)split * Cout + m0 + row] = t;
+    }
+  }
   float* S = slab + (size_t)split * Cout * Ktot;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -1741,6 +1804,16 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
     }
     reinterpret_cast<float4*>(out)[i] = s;
   }
+}
+
+// db = (accumulate ? db : 0) + sum_s db_slab[s], in split order (deterministic).
+__global__ void db_reduce_kernel(const float* __restrict__ db_slab, int splits, int C,
+                                 float* __restrict__ db, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = accumulate ? db[c] : 0.f;
+  for (int k = 0; k < splits; ++k) s += db_slab[(size_t)k * C + c];
+  db[c] = s;
 }
 
 // y = act(sum_s slab[s] + bias), summed in split order (deterministic).
@@ -1786,7 +1859,7 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
       const long long o = epi_out_index(epi, n, co, p / W, p % W, Cout, H, W);
       if (o >= 0) Y[o] = v;
     } else {
-      Y[idx] = v;
+      Y[idx] = epi_mask(epi, idx, v);
     }
   }
 }
@@ -2320,8 +2393,8 @@ struct WgradBs {
     const double chunk_s = 2.0 * C::BM * C::BN * C::TK * NP / (2516.6e12 * 0.5 / slots);
     return pick_splits_cost(tiles, chunks, slots, chunk_s, 4.0 * Cout * Cin * KS * KS);
   }
-  static int launch(const float* G, const float* X, float* slab, int splits, int N, int Cin,
-                    int H, int W, int Cout, hipStream_t s) {
+  static int launch(const float* G, const float* X, float* slab, float* db_slab, int splits,
+                    int N, int Cin, int H, int W, int Cout, hipStream_t s) {
     const int tiles_m = div_up(Cout, C::BM), tiles_n = div_up(Cin * KS * KS, C::BN);
     const int total_chunks = N * div_up(H * W, C::TK);
     const int cps = div_up(total_chunks, splits);
@@ -2334,7 +2407,7 @@ struct WgradBs {
       attr = true;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), C::LDS_BYTES, s, G, X, slab, N, Cin,
-                       H, W, Cout, tiles_m, tiles_n, splits, cps, 1.0f / (float)W);
+                       H, W, Cout, tiles_m, tiles_n, splits, cps, 1.0f / (float)W, db_slab);
     TLOD_LAUNCH_CHECK();
     return kOk;
   }
@@ -2461,15 +2534,22 @@ extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, i
   return kOk;
 }
 
+// workspace: the split slabs of dW, then (16-B aligned) the split slabs of db
+static size_t wgrad_bs_ws(int sp, int Cin, int Cout, int KS) {
+  return align_up((size_t)sp * Cout * Cin * KS * KS * sizeof(float), 16) +
+         (size_t)sp * Cout * sizeof(float);
+}
+
 extern "C" size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
                                                      int nprod) {
   const int sp = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
-  return sp > 0 ? (size_t)sp * Cout * Cin * KS * KS * sizeof(float) : 0;
+  return sp > 0 ? wgrad_bs_ws(sp, Cin, Cout, KS) : 0;
 }
 
-extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, int accumulate,
-                                      int N, int Cin, int H, int W, int Cout, int KS, int nprod,
-                                      void* ws, size_t ws_bytes, tlod_stream_t stream) {
+extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, float* db,
+                                      int accumulate, int N, int Cin, int H, int W, int Cout,
+                                      int KS, int nprod, void* ws, size_t ws_bytes,
+                                      tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
   TLOD_CHECK_ARG((Cout * Cin * KS * KS) % 4 == 0, "Cout*Cin*KS*KS must be a multiple of 4");
   TLOD_CHECK_ARG(KS == 1 || KS == 3, "conv wgrad: only 1x1 and 3x3 kernels");
@@ -2480,20 +2560,43 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
   hipStream_t s = (hipStream_t)stream;
   const int splits =
       with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
-  if (ws_bytes < (size_t)splits * Cout * Cin * KS * KS * sizeof(float)) {
+  if (ws_bytes < wgrad_bs_ws(splits, Cin, Cout, KS)) {
     set_error("tlod_conv_wgrad_bs_f32: workspace too small");
     return kWorkspace;
   }
   float* slab = static_cast<float*>(ws);
+  float* db_slab = db ? reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                                 align_up((size_t)splits * Cout * Cin * KS * KS *
+                                                              sizeof(float), 16))
+                      : nullptr;
   const int st = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) {
-    return cfg.launch(dy, x, slab, splits, N, Cin, H, W, Cout, s);
+    return cfg.launch(dy, x, slab, db_slab, splits, N, Cin, H, W, Cout, s);
   });
   if (st) return st;
   const size_t count = (size_t)Cout * Cin * KS * KS;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count / 4 + 255) / 256, 2048)),
                      dim3(256), 0, s, slab, splits, count, dw, accumulate);
   TLOD_LAUNCH_CHECK();
+  if (db) {
+    hipLaunchKernelGGL(db_reduce_kernel, dim3(div_up(Cout, 256)), dim3(256), 0, s, db_slab, splits,
+                       Cout, db, accumulate);
+    TLOD_LAUNCH_CHECK();
+  }
   return kOk;
+}
+
+// dx = dgrad(dy) * (mask > 0): tlod_conv_fwd_bs_f32's dgrad form with the previous layer's
+// ReLU backward in the epilogue (mask = that layer's ReLU output = this conv's input).
+extern "C" int tlod_conv_dgrad_bs_mask_f32(const float* dy, const void* wp, const float* mask,
+                                           float* dx, int N, int Cin, int H, int W, int Cout,
+                                           int nprod, void* ws, size_t ws_bytes,
+                                           tlod_stream_t stream) {
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0 && dy && wp && dx, "bad shape");
+  TLOD_CHECK_ARG(mask != dx, "mask must not alias dx");
+  Epi e{nullptr, nullptr, nullptr, 0};
+  e.mask = mask;
+  return conv_fwd_bs_dispatch(dy, (const unsigned short*)wp, e, dx, N, Cin, H, W, Cout, 3, nprod,
+                              (float*)ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int tlod_relu_bwd_bias_f32(const float* dy, const float* y, float* g, float* db,

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cfloat>
 
+#include <hipcub/hipcub.hpp>
+
 #include "common.h"
 #include "tlod.h"
 
@@ -307,6 +309,188 @@ __global__ void __launch_bounds__(kLdsThreads) roi_align_avg_bwd_lds_kernel(
   }
 }
 
+// ------------------------------------------------------------ RoIAlignAvg backward, gather
+// No atomics at all: the scatter (roi, sample, tap) -> feature cell is inverted once per call
+// and every (cell, channel) of bottom_grad is then a gather over its own contributions.
+//   1. geometry: one thread per (roi, sample): the four taps' cell ids (sentinel for a sample
+//      outside the map) and the sample's (hr, wr);
+//   2. a stable radix sort of the taps by cell (hipCUB), then each cell's start by binary
+//      search: the taps of a cell in ascending (roi, sample, tap) order — a fixed summation
+//      order, so the result is deterministic (the atomic kernels' is not);
+//   3. sample gradients sg[(roi, sample)][c] = avg_pool2d's backward of top_grad (the covering
+//      windows' top / 4, py outer, px inner — the atomic kernels' per-sample value), one
+//      coalesced (roi, sample) row of channels each;
+//   4. gather: a wave per 4 cells x 64 channels walks each cell's taps in sorted order — the
+//      tap list loaded 64 at a time across the lanes, broadcast by readlane, 16 sg rows in
+//      flight — applies roi_align_kernel.cu:137-140's per-tap weight and rounding, and the
+//      workgroup adds its 64 cells x 64 channels into NCHW bottom_grad through LDS (coalesced
+//      rows).
+// Traffic (DAF step: 556 RoIs x 64 samples x 512 channels, 2 x 37 x 75 map): top 56 MB read,
+// sg 73 MB written and read once per tap (~290 MB, mostly L2 / Infinity-Cache hits),
+// bottom_grad 11 MB read + written.
+constexpr int kGatherCells = 64, kGatherThreads = 1024;  // 16 waves x 4 cells
+
+__global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__ rois, int R,
+                                                       float scale, int H, int W, int ph, int pw,
+                                                       unsigned ncell,
+                                                       unsigned* __restrict__ keys,
+                                                       unsigned* __restrict__ vals,
+                                                       float2* __restrict__ geo) {
+  const int ah = ph + 1, aw = pw + 1, S = ah * aw;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * S) return;
+  const int r = i / S, smp = i % S, sy = smp / aw, sx = smp % aw;
+  const float* ro = rois + r * 5;
+  int y, x;
+  float hr, wr;
+  bool vy, vx;
+  align_axis(ro[2] * scale, ro[4] * scale, ah, sy, H, &y, &hr, &vy);
+  align_axis(ro[1] * scale, ro[3] * scale, aw, sx, W, &x, &wr, &vx);
+  const bool ok = vy && vx;
+  const unsigned c00 = (unsigned)(((int)ro[0] * H + y) * W + x);
+  geo[i] = make_float2(hr, wr);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    keys[4 * i + k] = ok ? c00 + (k >> 1) * W + (k & 1) : ncell;
+    vals[4 * i + k] = 4u * i + k;
+  }
+}
+
+// start[c] = first sorted tap of cell c (c = 0..ncell; start[ncell] = the valid tap count)
+__global__ void rbg_start_kernel(const unsigned* __restrict__ keys, int n, unsigned ncell,
+                                 int* __restrict__ start) {
+  const unsigned c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > ncell) return;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < c) lo = mid + 1; else hi = mid;
+  }
+  start[c] = lo;
+}
+
+// grid (R, ceil(C / 256)): sg[(r*S + s)*C + c]
+__global__ void __launch_bounds__(256) rbg_sample_grad_kernel(const float* __restrict__ top,
+                                                              int C, int ph, int pw,
+                                                              float* __restrict__ sg) {
+  const int ah = ph + 1, aw = pw + 1, S = ah * aw, P = ph * pw;
+  const int r = blockIdx.x, c0 = blockIdx.y * 256, t = threadIdx.x;
+  const int nc = min(256, C - c0);
+  __shared__ float g7[256 * 49];
+  const float* tp = top + ((size_t)r * C + c0) * P;
+  for (int e = t; e < nc * P; e += 256) g7[e] = tp[e] / 4.f;  // coalesced slab
+  __syncthreads();
+  if (t >= nc) return;
+  const float* gp = g7 + t * P;
+  float* o = sg + (size_t)r * S * C + c0 + t;
+  for (int sy = 0; sy < ah; ++sy)
+    for (int sx = 0; sx < aw; ++sx) {
+      float g = 0.f;  // avg_pool2d backward: py outer, px inner
+      for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
+        for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
+      o[(size_t)(sy * aw + sx) * C] = g;
+    }
+}
+
+// one tap's contribution, roi_align_kernel.cu:137-140 (as align_scatter)
+__device__ __forceinline__ float tap_value(float g, float hr, float wr, int k) {
+  const float om = 1.f - wr;
+  switch (k) {
+    case 0: return (float)(((double)g * (1. - (double)hr)) * (double)om);
+    case 1: return (float)(((double)g * (1. - (double)hr)) * (double)wr);
+    case 2: return (g * hr) * om;
+    default: return (g * hr) * wr;
+  }
+}
+
+// grid (ceil(ncell / 64), ceil(C / 64)); wave w: cells q0 + 4w .. + 3, lane = channel
+__global__ void __launch_bounds__(kGatherThreads) rbg_gather_kernel(
+    const int* __restrict__ start, const unsigned* __restrict__ vals,
+    const float2* __restrict__ geo, const float* __restrict__ sg, int C, int HW, int ncell,
+    float* __restrict__ grad) {
+  __shared__ float tile[kGatherCells][65];
+  const int q0 = blockIdx.x * kGatherCells, c0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = c0 + lane;
+  const bool cok = c < C;
+  constexpr int kPerWave = kGatherCells / (kGatherThreads / 64);
+  for (int ql = w * kPerWave; ql < w * kPerWave + kPerWave; ++ql) {
+    const int q = q0 + ql;
+    float acc = 0.f;
+    if (q < ncell) {
+      const int b = start[q], e = start[q + 1];
+      for (int j0 = b; j0 < e; j0 += 64) {
+        const int n = min(64, e - j0);
+        // the next <= 64 taps of the cell, one per lane
+        unsigned v = 0;
+        float2 gw = make_float2(0.f, 0.f);
+        if (lane < n) {
+          v = vals[j0 + lane];
+          gw = geo[v >> 2];
+        }
+        for (int j = 0; j < n; j += 16) {
+          float sv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
+            const unsigned vu = __builtin_amdgcn_readlane(v, min(j + u, n - 1));
+            sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            if (j + u >= n) break;
+            const unsigned vu = __builtin_amdgcn_readlane(v, j + u);
+            const float hr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gw.x), j + u));
+            const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gw.y), j + u));
+            acc += tap_value(sv[u], hr, wr, (int)(vu & 3));
+          }
+        }
+      }
+    }
+    tile[ql][lane] = acc;
+  }
+  __syncthreads();
+  // bottom_grad[b][c][p] += tile: lanes over 64 consecutive cells (coalesced rows)
+  for (int i = w; i < 64; i += kGatherThreads / 64) {
+    const int cc = c0 + i, q = q0 + lane;
+    if (cc < C && q < ncell) {
+      const int b = q / HW, p = q - b * HW;
+      grad[((size_t)b * C + cc) * HW + p] += tile[lane][i];
+    }
+  }
+}
+
+struct RbgWs {
+  unsigned *keys, *vals, *keys_s, *vals_s;
+  float2* geo;
+  int* start;
+  float* sg;
+  void* cub_tmp;
+  size_t cub_bytes;
+};
+
+static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, int ph, int pw) {
+  const size_t S = (size_t)(ph + 1) * (pw + 1), n = (size_t)R * S * 4;
+  w.keys = cv.take<unsigned>(n);
+  w.vals = cv.take<unsigned>(n);
+  w.keys_s = cv.take<unsigned>(n);
+  w.vals_s = cv.take<unsigned>(n);
+  w.geo = cv.take<float2>((size_t)R * S);
+  w.start = cv.take<int>((size_t)B * H * W + 1);
+  w.sg = cv.take<float>((size_t)R * S * C);
+  w.cub_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, w.cub_bytes, (const unsigned*)nullptr,
+                                           (unsigned*)nullptr, (const unsigned*)nullptr,
+                                           (unsigned*)nullptr, (int)n);
+  w.cub_tmp = cv.take<char>(w.cub_bytes);
+  return align_up(cv.off, 256);
+}
+
+static int rbg_bits(unsigned v) {  // bits needed for keys 0..v
+  int b = 1;
+  while (b < 32 && (v >> b)) ++b;
+  return b;
+}
+
 static size_t roi_lds_bytes(int H, int W, int R) {
   return (size_t)kLdsCh * H * W * sizeof(float) + (size_t)R * sizeof(int);
 }
@@ -425,6 +609,14 @@ extern "C" size_t tlod_roi_align_avg_bwd_workspace_bytes(int B, int C, int H, in
   return (size_t)B * C * H * W * sizeof(float);
 }
 
+extern "C" size_t tlod_roi_align_avg_bwd_gather_workspace_bytes(int B, int C, int H, int W, int R,
+                                                               int ph, int pw) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || R <= 0 || ph <= 0 || pw <= 0) return 0;
+  Carve cv(nullptr, 0);
+  RbgWs w;
+  return carve_rbg(cv, w, B, C, H, W, R, ph, pw);
+}
+
 extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W,
                                           const float* rois, int R, int ph, int pw, float scale,
                                           float* bottom_grad, void* ws, size_t ws_bytes,
@@ -433,6 +625,34 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
   TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
   if (R == 0) return kOk;
   hipStream_t s = (hipStream_t)stream;
+  const char* gv = getenv("TLOD_ROI_BWD_GATHER");  // opt-in (=1) until it wins; read per call
+  const bool gather_off = !(gv && *gv == '1');
+  const size_t ncell_sz = (size_t)B * H * W;
+  if (!gather_off && ws != nullptr && ncell_sz < (1u << 31) &&
+      ws_bytes >= tlod_roi_align_avg_bwd_gather_workspace_bytes(B, C, H, W, R, ph, pw)) {
+    Carve cv(ws, ws_bytes);
+    RbgWs w;
+    carve_rbg(cv, w, B, C, H, W, R, ph, pw);
+    const int S = (ph + 1) * (pw + 1), n = R * S * 4;
+    const unsigned ncell = (unsigned)ncell_sz;
+    hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale,
+                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo);
+    TLOD_LAUNCH_CHECK();
+    size_t cb = w.cub_bytes;
+    TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s,
+                                                n, 0, rbg_bits(ncell), s));
+    hipLaunchKernelGGL(rbg_start_kernel, dim3(div_up((int)ncell + 1, 256)), dim3(256), 0, s,
+                       w.keys_s, n, ncell, w.start);
+    TLOD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rbg_sample_grad_kernel, dim3(R, div_up(C, 256)), dim3(256), 0, s, top_grad,
+                       C, ph, pw, w.sg);
+    TLOD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rbg_gather_kernel, dim3(div_up((int)ncell, kGatherCells), div_up(C, 64)),
+                       dim3(kGatherThreads), 0, s, w.start, w.vals_s, w.geo, w.sg, C, H * W,
+                       (int)ncell, bottom_grad);
+    TLOD_LAUNCH_CHECK();
+    return kOk;
+  }
   static const bool lds_path = [] {
     const char* v = getenv("TLOD_ROI_BWD_LDS");  // opt-in: 1 = the LDS-accumulation kernel
     return v && *v == '1';

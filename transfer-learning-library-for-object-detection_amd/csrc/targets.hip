@@ -139,14 +139,27 @@ __device__ void block_random_subset(const int32_t* __restrict__ list, int n, int
       if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int need = s_need, acc = 0, d = 0;
-      for (; d < 256; ++d) {
-        if (acc + hist[d] >= need) break;
-        acc += hist[d];
+    if (threadIdx.x < 64) {
+      // the first digit d whose cumulative count reaches `need`: one wave, lane l owning
+      // digits 4l..4l+3 (a wave scan instead of a 256-step serial LDS walk on one lane —
+      // that walk was most of this kernel's time)
+      const int l = threadIdx.x, need = s_need;
+      const int h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2], h3 = hist[4 * l + 3];
+      const int sl = h0 + h1 + h2 + h3;
+      int incl = sl;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (l >= o) incl += y;
       }
-      s_need = need - acc;
-      s_prefix = prefix | ((uint32_t)d << shift);
+      int acc = incl - sl;
+      if (acc < need && need <= incl) {  // exactly one lane
+        int d = 4 * l;
+        if (acc + h0 < need) { acc += h0; ++d;
+          if (acc + h1 < need) { acc += h1; ++d;
+            if (acc + h2 < need) { acc += h2; ++d; } } }
+        s_need = need - acc;
+        s_prefix = prefix | ((uint32_t)d << shift);
+      }
     }
     __syncthreads();
   }

@@ -47,6 +47,8 @@ SIGNATURES = {
     "tlod_roi_align_avg_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
                                            c_float, P, P]),
     "tlod_roi_align_avg_bwd_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "tlod_roi_align_avg_bwd_gather_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int,
+                                                                 c_int, c_int]),
     "tlod_roi_align_avg_bwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
                                            c_float, P, P, c_size_t, P]),
     "tlod_roi_pool_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
@@ -96,14 +98,21 @@ SIGNATURES = {
                                      c_int, c_int, P, c_size_t, P]),
     "tlod_conv_wgrad_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
                                                       c_int]),
-    "tlod_conv_wgrad_bs_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                       c_int, P, c_size_t, P]),
+    "tlod_conv_wgrad_bs_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_int, P, c_size_t, P]),
+    "tlod_conv3x3_direct_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "tlod_conv_dgrad_bs_mask_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                            P, c_size_t, P]),
     "tlod_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "tlod_gemm_bs_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                  c_size_t, P]),
     "tlod_conv3x3_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
                                                         c_int]),
     "tlod_conv3x3_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
+                                         c_int, c_int, c_int, P, c_size_t, P]),
+    "tlod_conv1x1_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
+                                                        c_int]),
+    "tlod_conv1x1_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, P, c_size_t, P]),
     "tlod_maxpool2x2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_maxpool2x2_relu_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),

@@ -50,8 +50,10 @@ def conv_math():
                same normwise ~1e-7 vs fp64 as the f32-input MFMA; tests/test_conv_bs_gpu.py);
       "f32"  : the f32-input MFMA (exact f32 products);
       "bf16x3": 3 products (~5e-6 normwise), opt-in.
-    The 3x3 weight gradients follow it too (override: TLOD_WGRAD_MATH); 1x1 convs use the
-    f32-input MFMA in every mode."""
+    The 3x3 weight gradients follow it too (override: TLOD_WGRAD_MATH); 1x1 convs with >= 64
+    input and output channels (the ResNet bottlenecks, DA heads) run their forward / input
+    gradient on the split-bf16 conv GEMM too (_gemm1x1), narrower ones (RPN heads) on the
+    f32-input MFMA."""
     m = os.environ.get("TLOD_CONV_MATH", "bf16x6")
     if m not in MATHS:
         raise ValueError(f"TLOD_CONV_MATH={m!r}: expected one of {MATHS}")
@@ -79,7 +81,17 @@ def _gemm_conv(KS, math, out_channels):
             and os.environ.get("TLOD_CONV_GEMM", "0") != "0")
 
 
-def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind):
+def _gemm1x1(KS, math, cin, cout):
+    """1x1 convs under a split-bf16 math with >= 64 input and output channels run their
+    forward / input gradient as per-image GEMMs on the split-bf16 conv GEMM
+    (tlod_conv1x1_gemm_bs_f32: W (Cout x Cin) times the image's (Cin x HW) map, 64/128/256-row
+    tiles by Cout, the folded-BN / residual / ReLU epilogue); TLOD_CONV1X1_BS=0 keeps them on
+    the f32-input MFMA kernel."""
+    return (KS == 1 and math != "f32" and min(cin, cout) >= 64
+            and os.environ.get("TLOD_CONV1X1_BS", "1") != "0")
+
+
+def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS=3):
     N, Cin, H, W = x.shape
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
@@ -89,13 +101,16 @@ def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind):
         assert res.shape == y.shape, (res.shape, y.shape)
     L = _lib.lib()
     nprod = 6 if math == "bf16x6" else 3
-    ws = _lib.workspace(L.tlod_conv3x3_gemm_bs_workspace_bytes(N, Cin, H, W, Cout, w_layout, nprod),
-                        x.device, "conv")
-    shape = (N, Cin, H, W, Cout, 3) if kind == "fwd" else (N, Cout, H, W, Cin, 3)
+    wsb, fn, name = ((L.tlod_conv3x3_gemm_bs_workspace_bytes, L.tlod_conv3x3_gemm_bs_f32,
+                      "conv3x3_gemm_bs") if KS == 3 else
+                     (L.tlod_conv1x1_gemm_bs_workspace_bytes, L.tlod_conv1x1_gemm_bs_f32,
+                      "conv1x1_gemm_bs"))
+    ws = _lib.workspace(wsb(N, Cin, H, W, Cout, w_layout, nprod), x.device, "conv")
+    shape = (N, Cin, H, W, Cout, KS) if kind == "fwd" else (N, Cout, H, W, Cin, KS)
     _timed(kind, shape, lambda: _lib.check(
-        L.tlod_conv3x3_gemm_bs_f32(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc), _lib.ptr(b),
-                                   _lib.ptr(res), _lib.ptr(y), N, Cin, H, W, Cout, int(relu), nprod,
-                                   _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv3x3_gemm_bs"),
+        fn(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc), _lib.ptr(b), _lib.ptr(res),
+           _lib.ptr(y), N, Cin, H, W, Cout, int(relu), nprod, _lib.ptr(ws), ws.numel(),
+           _lib.stream_of(x)), name),
         math)
     return y
 
@@ -159,9 +174,14 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=Non
     N, Cin, H, W = x.shape
     Cout, _, KS, _ = weight.shape
     math = conv_math() if math is None else math
+    if KS == 3 and Cin <= 4 and scale is None and residual is None:
+        return _conv_direct(x, weight, bias, relu)
     if _gemm_conv(KS, math, Cout):
         return _conv_gemm(x, weight.detach().contiguous(), 0, bias, relu, scale, residual, Cout,
                           math, "fwd")
+    if _gemm1x1(KS, math, Cin, Cout):
+        return _conv_gemm(x, weight.detach().contiguous(), 0, bias, relu, scale, residual, Cout,
+                          math, "fwd", KS=1)
     if _bs(KS, math):
         return _conv_bs(x, pack_bs(weight, False) if wk is None else wk, bias, relu, scale,
                         residual, Cout, KS, math, "fwd")
@@ -178,6 +198,21 @@ def conv_fwd(x, weight, bias=None, relu=False, wk=None, scale=None, residual=Non
         L.tlod_conv_fwd_ex_f32(_lib.ptr(x), _lib.ptr(wk), _lib.ptr(sc), _lib.ptr(b),
                                _lib.ptr(res), _lib.ptr(y), N, Cin, H, W, Cout, KS, int(relu),
                                _lib.ptr(ws), ws.numel(), _lib.stream_of(x)), "conv_fwd"))
+    return y
+
+
+def _conv_direct(x, weight, bias, relu):
+    """3x3 convs with <= 4 input channels (VGG16 conv1_1 on the image): direct f32 FMA
+    kernel, one thread per output pixel (tlod_conv3x3_direct_f32) — the implicit GEMM would
+    pad K = 27 to a 72-deep chunk pair."""
+    N, Cin, H, W = x.shape
+    Cout = weight.shape[0]
+    y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
+    b = bias.detach().contiguous() if bias is not None else None
+    _timed("fwd", (N, Cin, H, W, Cout, 3), lambda: _lib.check(
+        _lib.lib().tlod_conv3x3_direct_f32(_lib.ptr(x), _lib.ptr(weight.detach().contiguous()),
+                                           _lib.ptr(b), _lib.ptr(y), N, Cin, H, W, Cout, int(relu),
+                                           _lib.stream_of(x)), "conv3x3_direct"), "f32")
     return y
 
 
@@ -199,13 +234,23 @@ def _conv_bs(x, wp, bias, relu, scale, residual, Cout, KS, math, kind):
     return y
 
 
-def conv_dgrad(g, weight, wd=None, math=None):
+def conv_dgrad(g, weight, wd=None, math=None, mask=None):
+    """Input gradient.  mask (the conv's input, when that is the previous conv's ReLU output):
+    on the split-bf16 3x3 path the result is dx * (mask > 0) — the previous layer's ReLU
+    backward done in this epilogue (tlod_conv_dgrad_bs_mask_f32) — and it is tagged so that
+    layer's backward skips its own pass (ConvFunction); other paths ignore mask."""
     g = g.contiguous()
     N, Cout, H, W = g.shape
     _, Cin, KS, _ = weight.shape
     math = conv_math() if math is None else math
+    if mask is not None and _bs(KS, math) and not _gemm_conv(KS, math, Cin):
+        return _conv_dgrad_mask(g, pack_bs(weight, True) if wd is None else wd, mask, Cin, math)
     if _gemm_conv(KS, math, Cin):
         return _conv_gemm(g, pack_dgrad(weight), 1, None, False, None, None, Cin, math, "dgrad")
+    if _gemm1x1(KS, math, Cout, Cin):
+        # dx = W^T g: the (Cout, Cin) weight read as the M-contiguous (M = Cin, K = Cout) operand
+        return _conv_gemm(g, weight.detach().contiguous(), 1, None, False, None, None, Cin, math,
+                          "dgrad", KS=1)
     if _bs(KS, math):
         # dgrad = the forward form over dy with the transposed, flipped pack
         return _conv_bs(g, pack_bs(weight, True) if wd is None else wd, None, False, None, None,
@@ -220,6 +265,29 @@ def conv_dgrad(g, weight, wd=None, math=None):
     return dx
 
 
+STATS = {"masked_dgrad": 0, "relu_bwd_skipped": 0}  # fused ReLU-backward counters (tests)
+
+
+def _conv_dgrad_mask(g, wp, mask, Cin, math):
+    N, Cout, H, W = g.shape
+    mask = mask.detach().contiguous()
+    assert mask.shape == (N, Cin, H, W), (mask.shape, g.shape)
+    dx = torch.empty((N, Cin, H, W), dtype=torch.float32, device=g.device)
+    L = _lib.lib()
+    nprod = 6 if math == "bf16x6" else 3
+    ws = _lib.workspace(L.tlod_conv_fwd_bs_workspace_bytes(N, Cout, H, W, Cin, 3, nprod), g.device,
+                        "conv")
+    _timed("dgrad", (N, Cin, H, W, Cout, 3), lambda: _lib.check(
+        L.tlod_conv_dgrad_bs_mask_f32(_lib.ptr(g), _lib.ptr(wp), _lib.ptr(mask), _lib.ptr(dx), N,
+                                      Cout, H, W, Cin, nprod, _lib.ptr(ws), ws.numel(),
+                                      _lib.stream_of(g)), "conv_dgrad_bs_mask"), math)
+    # the tag names the mask and this exact buffer state: autograd may sum another
+    # consumer's gradient into dx in place, which bumps _version and voids the tag
+    dx._tlod_relu_masked = (mask.data_ptr(), dx.data_ptr(), dx._version)
+    STATS["masked_dgrad"] += 1
+    return dx
+
+
 def wgrad_math():
     """Arithmetic of the 3x3 weight gradients (env TLOD_WGRAD_MATH, default: the
     TLOD_CONV_MATH choice): "bf16x6" / "bf16x3" run tlod_conv_wgrad_bs_f32 (split-bf16,
@@ -230,7 +298,10 @@ def wgrad_math():
     return m
 
 
-def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None):
+def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None, db=None):
+    """Weight gradient (into out when given).  db (Cout floats, optional): also the bias
+    gradient sum_{n,h,w} g, from the same launch on the split-bf16 path (the f32 path adds
+    a reduction pass)."""
     g = g.contiguous()
     x = x.contiguous()
     N, Cout, H, W = g.shape
@@ -244,10 +315,12 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None):
         ws = _lib.workspace(L.tlod_conv_wgrad_bs_workspace_bytes(N, Cin, H, W, Cout, KS, nprod),
                             g.device, "wgrad")
         _timed("wgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
-            L.tlod_conv_wgrad_bs_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin,
-                                     H, W, Cout, KS, nprod, _lib.ptr(ws), ws.numel(),
-                                     _lib.stream_of(g)), "conv_wgrad_bs"), math)
+            L.tlod_conv_wgrad_bs_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db),
+                                     int(accumulate), N, Cin, H, W, Cout, KS, nprod, _lib.ptr(ws),
+                                     ws.numel(), _lib.stream_of(g)), "conv_wgrad_bs"), math)
         return dw
+    if db is not None:
+        relu_bwd_bias(g, None, want_db=True, db_out=db)
     ws = _lib.workspace(L.tlod_conv_wgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "wgrad")
     _timed("wgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
         L.tlod_conv_wgrad_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), int(accumulate), N, Cin, H, W,
@@ -270,6 +343,34 @@ def relu_bwd_bias(dy, y=None, want_db=True, db_out=None):
     return g, db
 
 
+_FUSE_RELU = os.environ.get("TLOD_FUSE_RELU", "1") != "0"
+
+
+def _relu_out(x):
+    """x is the ReLU output of a ConvFunction (its ReLU backward can run in the next conv's
+    dgrad epilogue; TLOD_FUSE_RELU=0 disables that)."""
+    return _FUSE_RELU and getattr(x, "_tlod_relu_out", False)
+
+
+def _grad_relu(ctx, dy, y, need_b, need_w, bias):
+    """(g, db, db_via_wgrad) for a fused-ReLU conv's backward: g = dy * (y > 0).  When dy is
+    the next conv's dgrad already masked by y (conv_dgrad(mask=y), tagged) — and not a sum of
+    several consumers' gradients (a new tensor, or the tagged one added to in place: its
+    _version moved) — the ReLU backward pass is skipped and the bias gradient comes from
+    this conv's wgrad launch."""
+    if (y is not None and need_w and
+            getattr(dy, "_tlod_relu_masked", None) == (y.data_ptr(), dy.data_ptr(), dy._version)):
+        STATS["relu_bwd_skipped"] += 1
+        db = None
+        if need_b:
+            db = grad_out(bias)
+            if db is None:
+                db = torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device)
+        return dy, db, True
+    g, db = relu_bwd_bias(dy, y, want_db=need_b, db_out=grad_out(bias) if need_b else None)
+    return g, db, False
+
+
 class ConvFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu, tap=None):
@@ -279,7 +380,10 @@ class ConvFunction(torch.autograd.Function):
         ctx.relu = bool(relu)
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)  # gradient slots (tlod.grads)
+        ctx.mask_in = _relu_out(x)
         ctx.save_for_backward(x, weight, y if relu else None)
+        if relu:
+            y._tlod_relu_out = True
         return y
 
     @staticmethod
@@ -287,10 +391,10 @@ class ConvFunction(torch.autograd.Function):
         x, weight, y = ctx.saved_tensors
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], \
             ctx.has_bias and ctx.needs_input_grad[2]
-        g, db = relu_bwd_bias(dy, y if ctx.relu else None, want_db=need_b,
-                              db_out=grad_out(ctx.params[1]) if need_b else None)
-        dx = conv_dgrad(g, weight) if need_x else None
-        dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0])) if need_w else None
+        g, db, db_w = _grad_relu(ctx, dy, y if ctx.relu else None, need_b, need_w, ctx.params[1])
+        dx = conv_dgrad(g, weight, mask=x if ctx.mask_in else None) if need_x else None
+        dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0]),
+                        db=db if db_w else None) if need_w else None
         return dx, dw, db, None, None
 
 
@@ -391,6 +495,7 @@ class ConvPoolFunction(torch.autograd.Function):
             tap.append(y.detach().clone())
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
+        ctx.mask_in = _relu_out(x)
         ctx.save_for_backward(x, weight, y)
         return maxpool2x2(y)
 
@@ -401,7 +506,7 @@ class ConvPoolFunction(torch.autograd.Function):
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         g, db = maxpool_relu_bwd(dp, y, want_db=need_b,
                                  db_out=grad_out(ctx.params[1]) if need_b else None)
-        dx = conv_dgrad(g, weight) if need_x else None
+        dx = conv_dgrad(g, weight, mask=x if ctx.mask_in else None) if need_x else None
         dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.params[0])) if need_w else None
         return dx, dw, db, None
 

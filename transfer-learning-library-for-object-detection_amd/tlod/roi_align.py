@@ -70,7 +70,9 @@ class RoIAlignAvgFunction(torch.autograd.Function):
         g = grad_output.contiguous()
         grad_in = torch.zeros((B, C, H, W), dtype=g.dtype, device=g.device)
         L = _lib.lib()
-        ws = _lib.workspace(L.tlod_roi_align_avg_bwd_workspace_bytes(B, C, H, W), g.device,
+        R = rois_c.shape[0]
+        ws = _lib.workspace(max(L.tlod_roi_align_avg_bwd_gather_workspace_bytes(B, C, H, W, R, ph, pw),
+                                L.tlod_roi_align_avg_bwd_workspace_bytes(B, C, H, W)), g.device,
                             "roi_align_bwd")
         _lib.check(L.tlod_roi_align_avg_bwd_f32(
             _lib.ptr(g), B, C, H, W, _lib.ptr(rois_c), rois_c.shape[0], ph, pw, sc,
