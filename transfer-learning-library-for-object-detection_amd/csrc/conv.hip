@@ -1825,6 +1825,8 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
     const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tp,
     int th_rows, int tw_cols, int tiles_m, int tiles_w, int tiles_h, Epi epi, int Cout, int H,
     int W, float* __restrict__ Y, int band) {
+  // a thread takes 4 consecutive slab elements (one channel: tp is a multiple of 4) with one
+  // 16-B load per split piece; the channel's scale / bias once
   const int tile_elems = bm * tp;
   const int per_tile = (tile_elems + 1023) / 1024;
   const int ti = blockIdx.x / per_tile;
@@ -1835,31 +1837,42 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
   const int n = t;
   const size_t stride = (size_t)n_tail * tile_elems;
   const float* S = slab + (size_t)ti * tile_elems;
-  for (int e = (blockIdx.x % per_tile) * 1024 + threadIdx.x;
-       e < min(tile_elems, (blockIdx.x % per_tile + 1) * 1024); e += 256) {
-    const int ml = e / tp, pix = e % tp;
-    const int co = mt * bm + ml;
+  const int e0 = (blockIdx.x % per_tile) * 1024 + 4 * threadIdx.x;
+  if (e0 >= tile_elems) return;
+  const int ml = e0 / tp, pix0 = e0 % tp;
+  const int co = mt * bm + ml;
+  if (co >= Cout) return;
+  float4 v = *reinterpret_cast<const float4*>(S + e0);
+  for (int k = 1; k < ksplit; ++k) {
+    const float4 u = *reinterpret_cast<const float4*>(S + k * stride + e0);
+    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  }
+  const float sc = epi.scale ? epi.scale[co] : 1.f, bi = epi.bias ? epi.bias[co] : 0.f;
+  const float vv[4] = {v.x, v.y, v.z, v.w};
+  const size_t cbase = ((size_t)n * Cout + co) * (size_t)(H * W);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int pix = pix0 + e;
     int p;  // flattened pixel
     if (band) {
       p = tw * tp + pix;
-      if (co >= Cout || p >= H * W) continue;
+      if (p >= H * W) continue;
     } else {
       const int h = th * th_rows + pix / tw_cols, w = tw * tw_cols + pix % tw_cols;
-      if (co >= Cout || pix >= th_rows * tw_cols || h >= H || w >= W) continue;
+      if (pix >= th_rows * tw_cols || h >= H || w >= W) continue;
       p = h * W + w;
     }
-    float v = S[e];
-    for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
-    const size_t idx = ((size_t)n * Cout + co) * (size_t)(H * W) + p;
-    if (epi.scale) v *= epi.scale[co];
-    if (epi.bias) v += epi.bias[co];
-    if (epi.residual) v += epi.residual[idx];
-    if (epi.relu) v = fmaxf(v, 0.f);
+    const size_t idx = cbase + p;
+    float x = vv[e];
+    if (epi.scale) x *= sc;
+    x += bi;
+    if (epi.residual) x += epi.residual[idx];
+    if (epi.relu) x = fmaxf(x, 0.f);
     if (epi.s2d > 1) {
       const long long o = epi_out_index(epi, n, co, p / W, p % W, Cout, H, W);
-      if (o >= 0) Y[o] = v;
+      if (o >= 0) Y[o] = x;
     } else {
-      Y[idx] = epi_mask(epi, idx, v);
+      Y[idx] = epi_mask(epi, idx, x);
     }
   }
 }

@@ -336,6 +336,8 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
 __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
     const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tiles_m,
     int M, int N, const float* __restrict__ bias, float* __restrict__ C) {
+  // a thread takes 4 consecutive slab elements of one row (16-B loads per split piece; one
+  // 16-B store when the row is 16-B aligned in C)
   const int tile_elems = bm * kBN;
   const int per_tile = tile_elems / 1024;
   const int ti = blockIdx.x / per_tile;
@@ -343,13 +345,28 @@ __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
   const int mt = t % tiles_m, nt = t / tiles_m;
   const size_t stride = (size_t)n_tail * tile_elems;
   const float* S = slab + (size_t)ti * tile_elems;
-  const int e0 = (blockIdx.x % per_tile) * 1024;
-  for (int e = e0 + threadIdx.x; e < e0 + 1024; e += 256) {
-    const int m = mt * bm + e / kBN, n = nt * kBN + e % kBN;
-    if (m >= M || n >= N) continue;
-    float v = S[e];
-    for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
-    C[(size_t)m * N + n] = v + (bias ? bias[n] : 0.f);
+  const int e = (blockIdx.x % per_tile) * 1024 + 4 * threadIdx.x;
+  const int m = mt * bm + e / kBN, n = nt * kBN + e % kBN;
+  if (m >= M || n >= N) return;
+  float4 v = *reinterpret_cast<const float4*>(S + e);
+  for (int k = 1; k < ksplit; ++k) {
+    const float4 u = *reinterpret_cast<const float4*>(S + k * stride + e);
+    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  }
+  float* c = C + (size_t)m * N + n;
+  if (bias) {
+    v.x += bias[n];
+    if (n + 1 < N) v.y += bias[n + 1];
+    if (n + 2 < N) v.z += bias[n + 2];
+    if (n + 3 < N) v.w += bias[n + 3];
+  }
+  if (n + 3 < N && ((reinterpret_cast<uintptr_t>(c) & 15) == 0)) {
+    *reinterpret_cast<float4*>(c) = v;
+  } else {
+    c[0] = v.x;
+    if (n + 1 < N) c[1] = v.y;
+    if (n + 2 < N) c[2] = v.z;
+    if (n + 3 < N) c[3] = v.w;
   }
 }
 
