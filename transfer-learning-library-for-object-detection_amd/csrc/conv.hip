@@ -753,6 +753,12 @@ constexpr int kProdWaves = 4;
 #ifndef TLOD_WS_ROT
 #define TLOD_WS_ROT 1
 #endif
+#ifndef TLOD_WS_NOSTORE
+#define TLOD_WS_NOSTORE 0
+#endif
+#ifndef TLOD_WS_FRAME  // four-chunk frames of nine 16x16x32 steps (0: chunk pairs only)
+#define TLOD_WS_FRAME 1
+#endif
 #if TLOD_WS_STAMPS
 __device__ unsigned long long g_ws_stamps[256 * 12 * 10];
 __device__ unsigned long long g_ws_clock[512];
@@ -1049,7 +1055,23 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       WS_STAMP(8);
       __syncthreads();
       WS_STAMP(9);
-      for (int c = c_begin; c + 1 < c_end; c += 2) {
+      int c = c_begin;
+      // frames of four chunks (see the MFMA waves' loop): chunks c, c + 2 in buffer 0,
+      // c + 1, c + 3 in buffer 1; seven barriers
+      for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {
+        if (c != c_begin) store(smem + C::BUF);  // chunk c+1 (buffer 1 retired at F7)
+        __syncthreads();                          // F1: c+1 visible
+        __syncthreads();                          // F2: buffer 0 (chunk c) retired
+        store(smem);                              // chunk c+2
+        __syncthreads();                          // F3: c+2 visible
+        __syncthreads();                          // F4: buffer 1 (chunk c+1) retired
+        store(smem + C::BUF);                     // chunk c+3
+        __syncthreads();                          // F5: c+3 visible
+        __syncthreads();                          // F6: buffer 0 (chunk c+2) retired
+        if (c + 4 < c_end || (c + 4 == c_end && more)) store(smem);  // chunk c+4 / next item's first
+        __syncthreads();                          // F7: buffer 1 retired, c+4 visible
+      }
+      for (; c + 1 < c_end; c += 2) {
         WS_STAMP(-1);
         if (c != c_begin) store(smem + C::BUF);  // chunk c+1
         WS_STAMP(0);
@@ -1099,12 +1121,19 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
   };
   auto ua = [&](int u) { return (u >= 9 ? C::BUF : 0) + 16 * (u % 9); };
   auto ub = [&](int u) { return (u >= 9 ? C::BUF : 0) + tap_c(u % 9); };
-  int aoff[4], boff[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    aoff[s] = a_lane + ua(4 * s + g);
-    boff[s] = ub(4 * s + g);
-  }
+  // k-step s of a four-chunk frame: lane group g reads unit u = 4s + g of the frame's 36,
+  // i.e. chunk u / 9 (buffer (u / 9) & 1), tap u % 9; steps 0-3 are also the pair steps
+  // (computed per step from an opaque copy of g: nine hoisted offset pairs spill)
+  auto aoff_s = [&](int s) {
+    int gg = g;
+    asm volatile("" : "+v"(gg));
+    return a_lane + ua((4 * s + gg) % 18);
+  };
+  auto boff_s = [&](int s) {
+    int gg = g;
+    asm volatile("" : "+v"(gg));
+    return ub((4 * s + gg) % 18);
+  };
   const int hb = 8 * (g & 1);
   const int aoff4 = a_lane + ua(16 + (lane >> 5)) + hb;
   const int boff4 = ub(16 + (lane >> 5)) + hb;
@@ -1169,26 +1198,48 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     WS_STAMP(8);
     int c = it.c_begin;
     const int c_end = it.c_end;
+    // Four chunks (36 (tap, 8-channel) units) are nine 16x16x32 k-steps; a chunk pair's 18
+    // units leave a 16x16x16 step, which issues at the 16x16x32's 16 cycles for half the
+    // work (tools/probe/mfma_rate.hip), so whole frames run first.  Steps 2, 4 and 6 read
+    // two chunks (both buffers); a buffer is refilled once its chunk's last step is done.
+    for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {
+      step16(aoff_s(0), boff_s(0));
+      step16(aoff_s(1), boff_s(1));
+      __syncthreads();  // F1
+      step16(aoff_s(2), boff_s(2));
+      __syncthreads();  // F2
+      step16(aoff_s(3), boff_s(3));
+      __syncthreads();  // F3
+      step16(aoff_s(4), boff_s(4));
+      __syncthreads();  // F4
+      step16(aoff_s(5), boff_s(5));
+      __syncthreads();  // F5
+      step16(aoff_s(6), boff_s(6));
+      __syncthreads();  // F6
+      step16(aoff_s(7), boff_s(7));
+      step16(aoff_s(8), boff_s(8));
+      __syncthreads();  // F7
+    }
     for (; c + 1 < c_end; c += 2) {
       WS_STAMP(-1);
-      step16(aoff[0], boff[0]);
-      step16(aoff[1], boff[1]);
+      step16(aoff_s(0), boff_s(0));
+      step16(aoff_s(1), boff_s(1));
       WS_STAMP(0);
       __syncthreads();  // chunk c+1 visible
       WS_STAMP(1);
-      step16(aoff[2], boff[2]);
+      step16(aoff_s(2), boff_s(2));
       WS_STAMP(2);
       __syncthreads();  // buffer 0 retired
       WS_STAMP(3);
-      step16(aoff[3], boff[3]);
+      step16(aoff_s(3), boff_s(3));
       step8(aoff4, boff4);
       WS_STAMP(4);
       __syncthreads();
       WS_STAMP(5);
     }
     if (c < c_end) {
-      step16(aoff[0], boff[0]);
-      step16(aoff[1], boff[1]);
+      step16(aoff_s(0), boff_s(0));
+      step16(aoff_s(1), boff_s(1));
       step8(aoffL, boffL);
       __syncthreads();
     }
@@ -1287,6 +1338,9 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
               if (Rn) val += ext[cb][r];
               if (epi.relu) val = fmaxf(val, 0.f);
               if (Mn && !Rn && !(ext[cb][r] > 0.f)) val = 0.f;
+#if TLOD_WS_NOSTORE  // timing-only diagnostic build: the epilogue's stores skipped
+              if (val == 1234.5678f)
+#endif
               Yn[idx] = val;
             }
           }
@@ -2027,7 +2081,8 @@ static int resident_slots(K kern, int threads, size_t lds) {
 // through HBM.  Cost model in seconds: tiles at ~65% of the f32 MFMA peak per slot,
 // slab traffic (k writes + k reads + 1 write per tail tile) at 4 TB/s, 6 us per reduce.
 static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int nchunks,
-                             double tile_flops, int tile_elems, int slots, bool allow_split = true) {
+                             double tile_flops, int tile_elems, int slots, bool allow_split = true,
+                             int cps_align = 1) {
   FwdPlan p{tiles_m, tiles_w, tiles_h, 0, 1, nchunks, N};
   const long long T = (long long)tiles_m * tiles_w * tiles_h * N;
   p.dp_tiles = (int)T;
@@ -2037,8 +2092,9 @@ static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int n
   const int kmax = std::min(8, nchunks / 2);
   const long long q = T / slots;
   for (int k = 2; k <= kmax; ++k) {
-    const int cps = div_up(nchunks, k);
+    const int cps = div_up(div_up(nchunks, k), cps_align) * cps_align;
     const int kk = div_up(nchunks, cps);
+    if (kk < 2) continue;
     for (long long dp : {q * slots, 0ll}) {
       const long long tail = T - dp;
       if (tail <= 0) continue;
@@ -2155,7 +2211,8 @@ static bool use_band(int H, int W) {
 // build (TLOD_WS_FLAT == 0) has 32-bit offsets into one image.
 static bool use_ws(int Cin, int H, int W) {
   static const bool ws = tune_knob("TLOD_CONV_WS", 1) != 0;
-  return ws && Cin >= 128 && (TLOD_WS_FLAT != 0 || (size_t)Cin * H * W * 4 < (1ull << 31));
+  static const int min_cin = tune_knob("TLOD_WS_MINCIN", 128);
+  return ws && Cin >= min_cin && (TLOD_WS_FLAT != 0 || (size_t)Cin * H * W * 4 < (1ull << 31));
 }
 
 // Tile of the warp-specialized kernel for an H x W map: the fewest tiles of TH x TW <= 512
@@ -2211,9 +2268,11 @@ static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_sp
   // cost model in f32-MFMA-equivalent time: the split products run ~16/NP x faster
   const int tw = BAND ? div_up(H * W, C::TH * C::TW) : div_up(W, wt.tw);
   const int th = BAND ? 1 : div_up(H, wt.th);
+  // (warp-specialized pieces in whole four-chunk frames where the K allows)
   FwdPlan p = plan_schedule(div_up(Cout, C::BM), tw, th, N, nchunks,
                             2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
-                            C::BM * C::TH * C::TW, slots, allow_split);
+                            C::BM * C::TH * C::TW, slots, allow_split,
+                            ws && TLOD_WS_FRAME && nchunks >= 16 ? 4 : 1);
   if (ws) {
     p.th = wt.th;
     p.tw = wt.tw;
