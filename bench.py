@@ -47,6 +47,9 @@ def parse():
                     help="torch CPU threads of the baseline (the box's share of one GPU is 16)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--net", choices=("vgg16", "res101"), default="vgg16")
+    ap.add_argument("--classes", type=int, choices=(9, 21), default=None,
+                    help="9: Cityscapes (default), 21: PASCAL VOC (default for --method atf: "
+                         "BASELINE config 5, PASCAL->Clipart)")
     ap.add_argument("--method", choices=("daf", "maf", "atf"), default="daf",
                     help="detector (the headline metric is DAF; MAF / ATF are secondary workloads)")
     return ap.parse_args()
@@ -154,7 +157,12 @@ def main():
         local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    model = build_model(a.method, dev, a.net)
+    ncls = a.classes or (21 if a.method == "atf" else 9)
+    if ncls == 21:
+        from tlod.data.imdb import VOC_CLASSES
+        model = build_model(a.method, dev, a.net, classes=VOC_CLASSES, dataset="pascal_voc")
+    else:
+        model = build_model(a.method, dev, a.net)
     # clip_gradient(10) also for ResNet101 (the reference clips VGG16 only, DAF_train.py:406):
     # with random-init weights the unclipped first steps diverge; the fused step does the
     # same work either way (the norm is always computed)
@@ -210,12 +218,13 @@ def main():
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"{a.method.upper()} {a.net} Cityscapes->Foggy training step "
+        "config": {"workload": f"{a.method.upper()} {a.net} "
+                               f"{'PASCAL->Clipart' if ncls == 21 else 'Cityscapes->Foggy'} training step "
                                f"(methods/{a.method.upper()}/{a.method.upper()}_train.py), "
                                "1 source + 1 target image per GPU per step",
                    "image_hw": [a.height, a.width], "source_images_per_step": world,
                    "images_processed_per_step": 2 * world, "parallelism": f"dp{world}",
-                   "classes": 9, "rpn_pre_post_nms_train": [12000, 2000],
+                   "classes": ncls, "rpn_pre_post_nms_train": [12000, 2000],
                    "rpn_pre_post_nms_test": [6000, 300],
                    "rcnn_batch": 256 if a.net == "vgg16" else 128},
         "roofline": {"bound": "mfma", "achieved": round(dom["achieved"], 2),
@@ -242,7 +251,9 @@ def main():
                                   "gflop_per_step": round(conv_f / a.steps / 1e9, 2)},
                      "by_kind": detail},
         "conv_math": {"3x3 fwd/dgrad": tconv.conv_math(), "3x3 and 1x1 wgrad": tconv.wgrad_math(),
-                      "1x1 fwd/dgrad": "f32", "fc6/fc7/DA fc": linear_math()},
+                      "1x1 fwd/dgrad": f"{tconv.conv_math()} (>= 64 channels; f32 MFMA for "
+                                       "the RPN cls/bbox heads)",
+                      "fc6/fc7/DA fc": linear_math()},
         "mean_loss": round(last_loss, 4),
         # ReLU backward passes folded into the next conv's dgrad epilogue, per step (tlod.conv)
         "fused_relu_backward_per_step": {k: v / (a.steps + a.warmup)

@@ -16,6 +16,12 @@ python3 tools/pmc_traffic.py $O/fetch $O/write 13 $O/traffic.json > /dev/null
 timeout -k 10 120 python3 tools/bench_conv.py --math bf16x6 > $O/conv33.json 2> $O/conv33.err
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/conv33_stats -o run -- python3 tools/bench_conv.py --math bf16x6 > $O/conv33_rocprof.json 2> $O/conv33_stats.err
 TLOD_BENCH_SHAPES=1 timeout -k 10 200 $B > $O/bench_shapes.json 2> $O/bench_shapes.err
+# BASELINE configs 3-5 (per GPU): DAF ResNet101, MAF VGG16, ATF ResNet101 (21 classes)
+for cfg in "daf res101" "maf vgg16" "atf res101"; do
+  set -- $cfg
+  timeout -k 10 400 python3 bench.py --method $1 --net $2 --steps 10 --warmup 3 --cpu-baseline-steps 0 \
+    > $O/bench_$1_$2.json 2> $O/bench_$1_$2.err
+done
 if [ -n "$P" ]; then
   mkdir -p $P
   cp $O/traffic.json $P/traffic.json
@@ -24,5 +30,9 @@ if [ -n "$P" ]; then
   cp $O/conv33.json $P/conv33_bwd.json
   cp $O/conv33_stats/run_kernel_stats.csv $P/conv33_kernel_stats.csv
   cp $O/bench_rocprof.json $P/bench_line_rocprof.json
+  cp $O/bench_shapes.err $P/bench_conv_shapes.txt
+  for f in $O/bench_daf_res101.json $O/bench_maf_vgg16.json $O/bench_atf_res101.json; do
+    cp $f $P/
+  done
 fi
 cat $O/conv33.json
