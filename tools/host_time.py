@@ -1,6 +1,6 @@
 """Host-side (enqueue) time per training step vs the GPU step time: if the host needs about
 as long to issue a step as the GPU needs to run it, the GPU idles between launches.
-usage: python tools/host_time.py [steps]"""
+usage: python tools/host_time.py [steps] [net] [method]"""
 import os
 import sys
 import time
@@ -13,8 +13,10 @@ from tlod.detector.train import (SyntheticCityscapes, build_model, make_optimize
                                  train_step)
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+net = sys.argv[2] if len(sys.argv) > 2 else "vgg16"
+method = sys.argv[3] if len(sys.argv) > 3 else "daf"
 dev = torch.device("cuda", 0)
-model = build_model("daf", dev, "vgg16")
+model = build_model(method, dev, net)
 opt = make_optimizer(model, 2e-3, clip=10.0)
 data = SyntheticCityscapes(dev, H=600, W=1200, seed=1)
 for _ in range(5):

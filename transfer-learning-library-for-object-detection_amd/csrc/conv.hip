@@ -22,6 +22,7 @@
 #include "tlod.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 
 namespace tlod {
@@ -759,6 +760,9 @@ constexpr int kProdWaves = 4;
 #ifndef TLOD_WS_FRAME  // four-chunk frames of nine 16x16x32 steps (0: chunk pairs only)
 #define TLOD_WS_FRAME 1
 #endif
+#ifndef TLOD_WS_DEPTH2  // producers two chunks ahead in registers (one-item mode)
+#define TLOD_WS_DEPTH2 1
+#endif
 #if TLOD_WS_STAMPS
 __device__ unsigned long long g_ws_stamps[256 * 12 * 10];
 __device__ unsigned long long g_ws_clock[512];
@@ -962,6 +966,87 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       }
       x_rsrc = make_buffer_rsrc(X + (size_t)ld.n * Cin * HWi, (unsigned)Cin * HWi * 4u);
     };
+    if constexpr (!PERSIST && TLOD_WS_DEPTH2 && TLOD_WS_FLAT == 2) {
+      // One work item, two chunks in flight: chunk p of the item sits in register slot
+      // p & 1 (= its LDS buffer) from its load until its store, which then loads chunk
+      // p + 2 into the slot — a chunk's loads have two chunk-steps to land instead of one.
+      set_ld_item();
+      const int c_begin = ld.c_begin, c_end = ld.c_end;
+      unsigned am = 0, bm = 0;
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i) am |= (unsigned)(a_off[i] >= 0) << i;
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i) bm |= (unsigned)(b_goff[i] >= 0) << i;
+      const float* Xn = X + (size_t)ld.n * Cin * HWi;
+      u32x4 ra2[2][A_IT];
+      float rb2[2][B_IT][8];
+      int nv2[2] = {8, 8};
+      auto load2 = [&](auto slc, int ch) {  // chunk ch -> slot S (unconditional, masked at store)
+        constexpr int S = decltype(slc)::value;
+        const int ci0 = ch * C::CK;
+        const int nv = min(C::CK, Cin - ci0);
+        const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp) + ch * (kBsKP * 2);
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) ra2[S][i] = *reinterpret_cast<const u32x4*>(Wb + max(a_off[i], 0));
+        const float* Xc = Xn + (size_t)ci0 * HWi;
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rb2[S][i][e] = Xc[min(e, nv - 1) * HWi + max(b_goff[i], 0)];
+        nv2[S] = nv;
+      };
+      auto store2 = [&](auto slc, int ch_next) {  // slot S -> LDS buffer S; load ch_next into S
+        constexpr int S = decltype(slc)::value;
+        unsigned char* buf = smem + S * C::BUF;
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i)
+          if (a_lds[i] >= 0)
+            *reinterpret_cast<u32x4*>(buf + a_lds[i]) = ((am >> i) & 1) ? ra2[S][i] : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) {
+          if (b_pos[i] < 0) continue;
+          u32x4 sp[3];
+          float v8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v8[e] = (((bm >> i) & 1) && e < nv2[S]) ? rb2[S][i][e] : 0.f;
+          split8<C::NPL>(v8, sp);
+#pragma unroll
+          for (int pl = 0; pl < C::NPL; ++pl)
+            *reinterpret_cast<u32x4*>(buf + b_pos[i] + pl * C::B_PLANE) = sp[pl];
+        }
+        if (ch_next < c_end) load2(slc, ch_next);
+      };
+      const std::integral_constant<int, 0> S0;
+      const std::integral_constant<int, 1> S1;
+      load2(S0, c_begin);
+      if (c_begin + 1 < c_end) load2(S1, c_begin + 1);
+      store2(S0, c_begin + 2);                          // chunk c_begin
+      if (c_end - c_begin >= 2) store2(S1, c_begin + 3);  // chunk c_begin + 1
+      __syncthreads();
+      int c = c_begin;
+      for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {  // barriers as in the loop below
+        if (c != c_begin) store2(S1, c + 3);  // chunk c+1
+        __syncthreads();
+        __syncthreads();
+        store2(S0, c + 4);  // chunk c+2
+        __syncthreads();
+        __syncthreads();
+        store2(S1, c + 5);  // chunk c+3
+        __syncthreads();
+        __syncthreads();
+        if (c + 4 < c_end) store2(S0, c + 6);  // chunk c+4
+        __syncthreads();
+      }
+      for (; c + 1 < c_end; c += 2) {
+        if (c != c_begin) store2(S1, c + 3);  // chunk c+1
+        __syncthreads();
+        __syncthreads();
+        if (c + 2 < c_end) store2(S0, c + 4);  // chunk c+2
+        __syncthreads();
+      }
+      if ((c_end - c_begin) & 1) __syncthreads();
+      return;
+    }
     u32x4 ra[A_IT];
     float rb[B_IT][8];
     int ld_nv = 8;

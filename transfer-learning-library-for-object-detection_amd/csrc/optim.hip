@@ -12,6 +12,10 @@
 #include "common.h"
 #include "tlod.h"
 
+#ifndef TLOD_SGD_NT
+#define TLOD_SGD_NT 1
+#endif
+
 namespace tlod {
 
 static_assert(sizeof(tlod_sgd_chunk) == 48, "descriptor layout (tlod/optim.py _DESC)");
@@ -29,12 +33,13 @@ __global__ void __launch_bounds__(256) sgd_sumsq_kernel(const tlod_sgd_chunk* __
   const tlod_sgd_chunk c = chunks[blockIdx.x];
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (vec4_ok(c.grad, c.grad, c.grad, c.count)) {
-    const float4* g4 = reinterpret_cast<const float4*>(c.grad);
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const v4* g4 = reinterpret_cast<const v4*>(c.grad);
     const long long n4 = c.count / 4;
 #pragma unroll 4
     for (long long i = threadIdx.x; i < n4; i += 256) {
-      float4 g = g4[i];
-      g.x *= gs; g.y *= gs; g.z *= gs; g.w *= gs;
+      v4 g = g4[i];  // (a plain load: the update pass re-reads g, partly from the MALL)
+      g *= gs;
       s0 += g.x * g.x; s1 += g.y * g.y; s2 += g.z * g.z; s3 += g.w * g.w;
     }
   } else {
@@ -83,10 +88,32 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
   if (c.active != nullptr && *c.active == 0.f) return;  // no rank produced this gradient
   const float scale = norm_scale[1];
   if (vec4_ok(c.grad, c.param, c.momentum_buf, c.count)) {
+    const long long n4 = c.count / 4;
+#if TLOD_SGD_NT
+    // streaming: every element is touched once per step, ~15 ms and >10 GB of other traffic
+    // apart, so the loads and stores bypass the caches' retention (nontemporal)
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const v4* gv = reinterpret_cast<const v4*>(c.grad);
+    v4* pv = reinterpret_cast<v4*>(c.param);
+    v4* bv = reinterpret_cast<v4*>(c.momentum_buf);
+#pragma unroll 4
+    for (long long i = threadIdx.x; i < n4; i += 256) {
+      const v4 g = __builtin_nontemporal_load(gv + i);
+      v4 p = __builtin_nontemporal_load(pv + i), b = __builtin_nontemporal_load(bv + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = p[e], be = b[e];
+        sgd1(g[e], pe, be, gs, scale, c.weight_decay, c.lr, momentum);
+        p[e] = pe;
+        b[e] = be;
+      }
+      __builtin_nontemporal_store(b, bv + i);
+      __builtin_nontemporal_store(p, pv + i);
+    }
+#else
     const float4* __restrict__ g4 = reinterpret_cast<const float4*>(c.grad);
     float4* __restrict__ p4 = reinterpret_cast<float4*>(c.param);
     float4* __restrict__ b4 = reinterpret_cast<float4*>(c.momentum_buf);
-    const long long n4 = c.count / 4;
 #pragma unroll 2
     for (long long i = threadIdx.x; i < n4; i += 256) {
       const float4 g = g4[i];
@@ -98,6 +125,7 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
       b4[i] = b;
       p4[i] = p;
     }
+#endif
     return;
   }
   for (long long i = threadIdx.x; i < c.count; i += 256) {
