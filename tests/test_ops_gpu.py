@@ -84,14 +84,16 @@ def test_roi_align_fwd_bwd(B, C, H, W, R, ah, aw):
     np.testing.assert_allclose(ft.grad.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("path", ["gather", "atomic"])
 @pytest.mark.parametrize("B,C,H,W,R", [(1, 512, 37, 62, 256), (1, 100, 37, 75, 300), (2, 64, 12, 16, 33),
                                        (2, 33, 37, 75, 556), (2, 8, 100, 120, 60)])
-def test_roi_align_avg_fused(B, C, H, W, R):
+def test_roi_align_avg_fused(B, C, H, W, R, path, monkeypatch):
     """Odd C, RoIs of two images interleaved; (2, 33, 37, 75, 556) is the DAF step's RoI
-    count on its base-feature map (the opt-in LDS-accumulation backward, TLOD_ROI_BWD_LDS=1,
-    passed these cases too; (2, 8, 100, 120) is beyond its 64 KB and takes the atomic
-    kernels)."""
+    count on its base-feature map; backward through the default sorted-tap gather and the
+    atomic kernels (TLOD_ROI_BWD_GATHER=0; the opt-in LDS-accumulation backward,
+    TLOD_ROI_BWD_LDS=1, passed these cases too)."""
     from tlod.roi_align import RoIAlignAvg
+    monkeypatch.setenv("TLOD_ROI_BWD_GATHER", "1" if path == "gather" else "0")
     rng = np.random.default_rng(R)
     f = _feat(rng, B, C, H, W)
     r = _rois(rng, R, B, W * 16, H * 16)
@@ -106,16 +108,23 @@ def test_roi_align_avg_fused(B, C, H, W, R):
 
 
 @pytest.mark.parametrize("B,C,H,W,R,P", [(2, 512, 37, 75, 556, 7), (1, 40, 20, 30, 90, 3),
-                                         (2, 16, 6, 5, 17, 7)])
+                                         (2, 16, 6, 5, 17, 7), (1, 70, 20, 30, -300, 7)])
 def test_roi_align_avg_bwd_gather(B, C, H, W, R, P, monkeypatch):
-    """The gather backward (TLOD_ROI_BWD_GATHER=1: taps sorted by feature cell, no atomics) is
-    deterministic — two calls bit-identical — and matches the oracle to 1e-5; (2, 16, 6, 5):
-    RoIs past the map (invalid samples)."""
+    """The gather backward (taps sorted by feature cell, no atomics) is deterministic — two
+    calls bit-identical — and matches the oracle to 1e-5; (2, 16, 6, 5): RoIs past the map
+    (invalid samples); R = -300: 300 copies of one small RoI, so a few cells take thousands
+    of taps whose runs cross many 64-tap segments (the carry / fixup chain)."""
     from tlod.roi_align import RoIAlignAvg
     monkeypatch.setenv("TLOD_ROI_BWD_GATHER", "1")
-    rng = np.random.default_rng(R + P)
+    rng = np.random.default_rng(abs(R) + P)
     f = _feat(rng, B, C, H, W)
-    r = _rois(rng, R, B, W * 16 + 200, H * 16 + 200)
+    atol = 1e-5
+    if R < 0:
+        r = np.tile(np.array([[0, 100.0, 90.0, 130.0, 121.0]], np.float32), (-R, 1))
+        R = -R
+        atol = 1e-4  # ~8k-term sums (partials ~10x the result) in another order than the oracle
+    else:
+        r = _rois(rng, R, B, W * 16 + 200, H * 16 + 200)
     g = rng.standard_normal((R, C, P, P)).astype(np.float32)
 
     def grad():
@@ -126,7 +135,7 @@ def test_roi_align_avg_bwd_gather(B, C, H, W, R, P, monkeypatch):
     a, b = grad(), grad()
     np.testing.assert_array_equal(a, b)
     ref = oroi.roi_align_avg_bwd(g, r, B, C, H, W, 1.0 / 16)
-    np.testing.assert_allclose(a, ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(a, ref, rtol=1e-5, atol=atol)
 
 
 @pytest.mark.parametrize("B,C,H,W,R", [(1, 64, 37, 62, 128), (2, 16, 20, 25, 40)])

@@ -49,8 +49,9 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / 20 * 1e3
-    kind = ("gather" if os.environ.get("TLOD_ROI_BWD_GATHER") == "1" else
-            "lds" if os.environ.get("TLOD_ROI_BWD_LDS") == "1" else "atomic")
+    kind = ("atomic" if os.environ.get("TLOD_ROI_BWD_GATHER") == "0" and
+            os.environ.get("TLOD_ROI_BWD_LDS") != "1" else
+            "lds" if os.environ.get("TLOD_ROI_BWD_GATHER") == "0" else "gather")
     print(json.dumps({"kernel": kind, "roi_align_avg_bwd_us": round(us, 1),
                       "R": R, "C": C, "map": [H, W]}))
 

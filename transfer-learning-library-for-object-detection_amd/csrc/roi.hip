@@ -320,15 +320,17 @@ __global__ void __launch_bounds__(kLdsThreads) roi_align_avg_bwd_lds_kernel(
 //   3. sample gradients sg[(roi, sample)][c] = avg_pool2d's backward of top_grad (the covering
 //      windows' top / 4, py outer, px inner — the atomic kernels' per-sample value), one
 //      coalesced (roi, sample) row of channels each;
-//   4. gather: a wave per 4 cells x 64 channels walks each cell's taps in sorted order — the
-//      tap list loaded 64 at a time across the lanes, broadcast by readlane, 16 sg rows in
-//      flight — applies roi_align_kernel.cu:137-140's per-tap weight and rounding, and the
-//      workgroup adds its 64 cells x 64 channels into NCHW bottom_grad through LDS (coalesced
-//      rows).
+//   4. gather, balanced by taps: a wave takes 64 consecutive sorted taps x 64 channels (lane =
+//      channel; keys / tap ids broadcast by readlane, 16 sg rows in flight), applies
+//      roi_align_kernel.cu:137-140's per-tap weight and rounding, and sums each run of equal
+//      cells in order.  A run inside the segment is stored to a channels-last accumulator; a
+//      run crossing segment boundaries leaves its pieces (the segment's head / tail run) in
+//      carry rows, which a fixup pass adds in segment order (the run's first segment owns it);
+//      then one tiled pass adds the accumulator into NCHW bottom_grad.  (Round 3's first
+//      version gave each wave 4 cells: the cells under many RoIs serialized it, 114 us.)
 // Traffic (DAF step: 556 RoIs x 64 samples x 512 channels, 2 x 37 x 75 map): top 56 MB read,
 // sg 73 MB written and read once per tap (~290 MB, mostly L2 / Infinity-Cache hits),
 // bottom_grad 11 MB read + written.
-constexpr int kGatherCells = 64, kGatherThreads = 1024;  // 16 waves x 4 cells
 
 __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__ rois, int R,
                                                        float scale, int H, int W, int ph, int pw,
@@ -369,27 +371,29 @@ __global__ void rbg_start_kernel(const unsigned* __restrict__ keys, int n, unsig
   start[c] = lo;
 }
 
-// grid (R, ceil(C / 256)): sg[(r*S + s)*C + c]
+// grid (R, ceil(C / 64)), 256 threads: sg[(r*S + s)*C + c]; thread (part = t / 64, channel
+// t % 64) writes samples part, part + 4, ... (a 256-B row of channels per sample and wave)
 __global__ void __launch_bounds__(256) rbg_sample_grad_kernel(const float* __restrict__ top,
                                                               int C, int ph, int pw,
                                                               float* __restrict__ sg) {
   const int ah = ph + 1, aw = pw + 1, S = ah * aw, P = ph * pw;
-  const int r = blockIdx.x, c0 = blockIdx.y * 256, t = threadIdx.x;
-  const int nc = min(256, C - c0);
-  __shared__ float g7[256 * 49];
+  const int r = blockIdx.x, c0 = blockIdx.y * 64, t = threadIdx.x;
+  const int nc = min(64, C - c0);
+  __shared__ float g7[64 * 49];
   const float* tp = top + ((size_t)r * C + c0) * P;
   for (int e = t; e < nc * P; e += 256) g7[e] = tp[e] / 4.f;  // coalesced slab
   __syncthreads();
-  if (t >= nc) return;
-  const float* gp = g7 + t * P;
-  float* o = sg + (size_t)r * S * C + c0 + t;
-  for (int sy = 0; sy < ah; ++sy)
-    for (int sx = 0; sx < aw; ++sx) {
-      float g = 0.f;  // avg_pool2d backward: py outer, px inner
-      for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
-        for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
-      o[(size_t)(sy * aw + sx) * C] = g;
-    }
+  const int ch = t & 63;
+  if (ch >= nc) return;
+  const float* gp = g7 + ch * P;
+  float* o = sg + (size_t)r * S * C + c0 + ch;
+  for (int smp = t >> 6; smp < S; smp += 4) {
+    const int sy = smp / aw, sx = smp % aw;
+    float g = 0.f;  // avg_pool2d backward: py outer, px inner
+    for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
+      for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
+    o[(size_t)smp * C] = g;
+  }
 }
 
 // one tap's contribution, roi_align_kernel.cu:137-140 (as align_scatter)
@@ -403,67 +407,97 @@ __device__ __forceinline__ float tap_value(float g, float hr, float wr, int k) {
   }
 }
 
-// grid (ceil(ncell / 64), ceil(C / 64)); wave w: cells q0 + 4w .. + 3, lane = channel
-__global__ void __launch_bounds__(kGatherThreads) rbg_gather_kernel(
-    const int* __restrict__ start, const unsigned* __restrict__ vals,
-    const float2* __restrict__ geo, const float* __restrict__ sg, int C, int HW, int ncell,
-    float* __restrict__ grad) {
-  __shared__ float tile[kGatherCells][65];
-  const int q0 = blockIdx.x * kGatherCells, c0 = blockIdx.y * 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = c0 + lane;
+// grid (ceil(nseg / 4), ceil(C / 64)), 4 waves: wave = segment of 64 sorted taps, lane =
+// channel.  flags[seg]: 1 = owns a run continuing into the next segments (its tail piece in
+// carry_tail), 2 = one run covering the whole segment and continuing on both sides.
+__global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
+    const int* __restrict__ start, const unsigned* __restrict__ keys,
+    const unsigned* __restrict__ vals, const float2* __restrict__ geo,
+    const float* __restrict__ sg, int C, int ncell, float* __restrict__ acc,
+    float* __restrict__ carry_head, float* __restrict__ carry_tail, int* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = start[ncell];  // valid taps (sorted to the front)
+  const int j0 = seg * 64;
+  if (j0 >= n) return;
+  const int jn = min(64, n - j0);
+  const int c = blockIdx.y * 64 + lane;
   const bool cok = c < C;
-  constexpr int kPerWave = kGatherCells / (kGatherThreads / 64);
-  for (int ql = w * kPerWave; ql < w * kPerWave + kPerWave; ++ql) {
-    const int q = q0 + ql;
-    float acc = 0.f;
-    if (q < ncell) {
-      const int b = start[q], e = start[q + 1];
-      for (int j0 = b; j0 < e; j0 += 64) {
-        const int n = min(64, e - j0);
-        // the next <= 64 taps of the cell, one per lane
-        unsigned v = 0;
-        float2 gw = make_float2(0.f, 0.f);
-        if (lane < n) {
-          v = vals[j0 + lane];
-          gw = geo[v >> 2];
-        }
-        for (int j = 0; j < n; j += 16) {
-          float sv[16];
+  unsigned kl = 0xffffffffu, vl = 0;
+  float2 gl = make_float2(0.f, 0.f);
+  if (lane < jn) {
+    kl = keys[j0 + lane];
+    vl = vals[j0 + lane];
+    gl = geo[vl >> 2];
+  }
+  const unsigned kprev = j0 > 0 ? keys[j0 - 1] : 0xffffffffu;
+  const unsigned knext = j0 + jn < n ? keys[j0 + jn] : 0xffffffffu;
+  unsigned cur = __builtin_amdgcn_readfirstlane(kl);
+  int runs = 0;
+  float a = 0.f;
+  auto flush = [&](bool last) {
+    const bool cont_prev = runs == 0 && cur == kprev;
+    const bool cont_next = last && cur == knext;
+    if (cok) {
+      if (cont_prev) carry_head[(size_t)seg * C + c] = a;
+      else if (cont_next) carry_tail[(size_t)seg * C + c] = a;
+      else acc[(size_t)cur * C + c] = a;
+    }
+    if (last && blockIdx.y == 0 && lane == 0)
+      flags[seg] = (cont_next && !cont_prev ? 1 : 0) | (runs == 0 && cont_prev && cont_next ? 2 : 0);
+    ++runs;
+  };
+  for (int j = 0; j < jn; j += 16) {
+    float sv[16];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
-            const unsigned vu = __builtin_amdgcn_readlane(v, min(j + u, n - 1));
-            sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
-          }
+    for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
+      const unsigned vu = __builtin_amdgcn_readlane(vl, min(j + u, jn - 1));
+      sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
+    }
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            if (j + u >= n) break;
-            const unsigned vu = __builtin_amdgcn_readlane(v, j + u);
-            const float hr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gw.x), j + u));
-            const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gw.y), j + u));
-            acc += tap_value(sv[u], hr, wr, (int)(vu & 3));
-          }
-        }
+    for (int u = 0; u < 16; ++u) {
+      if (j + u >= jn) break;
+      const unsigned ku = __builtin_amdgcn_readlane(kl, j + u);
+      if (ku != cur) {
+        flush(false);
+        cur = ku;
+        a = 0.f;
       }
-    }
-    tile[ql][lane] = acc;
-  }
-  __syncthreads();
-  // bottom_grad[b][c][p] += tile: lanes over 64 consecutive cells (coalesced rows)
-  for (int i = w; i < 64; i += kGatherThreads / 64) {
-    const int cc = c0 + i, q = q0 + lane;
-    if (cc < C && q < ncell) {
-      const int b = q / HW, p = q - b * HW;
-      grad[((size_t)b * C + cc) * HW + p] += tile[lane][i];
+      const unsigned vu = __builtin_amdgcn_readlane(vl, j + u);
+      const float hr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl.x), j + u));
+      const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl.y), j + u));
+      a += tap_value(sv[u], hr, wr, (int)(vu & 3));
     }
   }
+  flush(true);
+}
+
+// the runs crossing segments: the owning segment's tail piece, then the next segments' head
+// pieces in order (deterministic)
+__global__ void __launch_bounds__(256) rbg_seg_fixup_kernel(
+    const int* __restrict__ start, const unsigned* __restrict__ keys, int C, int ncell,
+    const float* __restrict__ carry_head, const float* __restrict__ carry_tail,
+    const int* __restrict__ flags, float* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = start[ncell];
+  if (seg * 64 >= n || !(flags[seg] & 1)) return;
+  const int c = blockIdx.y * 64 + lane;
+  if (c >= C) return;
+  const unsigned cell = keys[min(seg * 64 + 64, n) - 1];
+  float a = carry_tail[(size_t)seg * C + c];
+  for (int k = seg + 1; k * 64 < n; ++k) {
+    a += carry_head[(size_t)k * C + c];
+    if (!(flags[k] & 2)) break;
+  }
+  acc[(size_t)cell * C + c] = a;
 }
 
 struct RbgWs {
   unsigned *keys, *vals, *keys_s, *vals_s;
   float2* geo;
-  int* start;
-  float* sg;
+  int *start, *flags;
+  float *sg, *acc, *carry_head, *carry_tail;
   void* cub_tmp;
   size_t cub_bytes;
 };
@@ -477,6 +511,11 @@ static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, 
   w.geo = cv.take<float2>((size_t)R * S);
   w.start = cv.take<int>((size_t)B * H * W + 1);
   w.sg = cv.take<float>((size_t)R * S * C);
+  const size_t nseg = (n + 63) / 64;
+  w.acc = cv.take<float>((size_t)B * H * W * C);
+  w.carry_head = cv.take<float>(nseg * C);
+  w.carry_tail = cv.take<float>(nseg * C);
+  w.flags = cv.take<int>(nseg);
   w.cub_bytes = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, w.cub_bytes, (const unsigned*)nullptr,
                                            (unsigned*)nullptr, (const unsigned*)nullptr,
@@ -625,8 +664,10 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
   TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
   if (R == 0) return kOk;
   hipStream_t s = (hipStream_t)stream;
-  const char* gv = getenv("TLOD_ROI_BWD_GATHER");  // opt-in (=1) until it wins; read per call
-  const bool gather_off = !(gv && *gv == '1');
+  // the sorted-tap gather by default (177 vs 243 us on the DAF step's RoIs, deterministic);
+  // TLOD_ROI_BWD_GATHER=0: the atomic kernels (read per call)
+  const char* gv = getenv("TLOD_ROI_BWD_GATHER");
+  const bool gather_off = gv && *gv == '0';
   const size_t ncell_sz = (size_t)B * H * W;
   if (!gather_off && ws != nullptr && ncell_sz < (1u << 31) &&
       ws_bytes >= tlod_roi_align_avg_bwd_gather_workspace_bytes(B, C, H, W, R, ph, pw)) {
@@ -644,12 +685,20 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     hipLaunchKernelGGL(rbg_start_kernel, dim3(div_up((int)ncell + 1, 256)), dim3(256), 0, s,
                        w.keys_s, n, ncell, w.start);
     TLOD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(rbg_sample_grad_kernel, dim3(R, div_up(C, 256)), dim3(256), 0, s, top_grad,
+    hipLaunchKernelGGL(rbg_sample_grad_kernel, dim3(R, div_up(C, 64)), dim3(256), 0, s, top_grad,
                        C, ph, pw, w.sg);
     TLOD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(rbg_gather_kernel, dim3(div_up((int)ncell, kGatherCells), div_up(C, 64)),
-                       dim3(kGatherThreads), 0, s, w.start, w.vals_s, w.geo, w.sg, C, H * W,
-                       (int)ncell, bottom_grad);
+    TLOD_HIP(hipMemsetAsync(w.acc, 0, ncell_sz * C * sizeof(float), s));
+    const int nseg = div_up(n, 64);
+    hipLaunchKernelGGL(rbg_seg_gather_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
+                       w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell, w.acc,
+                       w.carry_head, w.carry_tail, w.flags);
+    TLOD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
+                       w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
+    TLOD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
+                       0, s, w.acc, C, H * W, bottom_grad);
     TLOD_LAUNCH_CHECK();
     return kOk;
   }
