@@ -1,7 +1,7 @@
 """Microbenchmark: RoIAlignAvg 7x7 backward on the DAF step's shape (2 images, base feature
-512 x 37 x 75, 256 source + 300 target RoIs of realistic sizes): the default gather
-backward: the global-atomic NHWC kernel (default), TLOD_ROI_BWD_GATHER=1 the gather kernel
-(sorted taps, no atomics), TLOD_ROI_BWD_LDS=1 the LDS-accumulation kernel."""
+512 x 37 x 75, 256 source + 300 target RoIs of realistic sizes): the sorted-tap gather
+(default, no atomics), TLOD_ROI_BWD_GATHER=0 the global-atomic NHWC kernel,
+TLOD_ROI_BWD_GATHER=0 TLOD_ROI_BWD_LDS=1 the LDS-accumulation kernel."""
 import json
 import os
 import sys
