@@ -358,6 +358,14 @@ int tlod_subsample2_f32(const float* x, int N, int C, int H, int W, float* y,
                         tlod_stream_t stream);
 int tlod_upsample2_zero_f32(const float* dy, int N, int C, int H, int W, float* dx,
                             tlod_stream_t stream);
+/* RoI head (layer4 on R RoI maps, lib/DAF/resnet.py:64-102 applied by RCNN_top, :277-288)
+ * channels-last 3x3 convs as GEMMs: col[(r,h,w)][(kh,kw,c)] = x[r][h+kh-1][w+kw-1][c]
+ * (zero padding 1), x (R,H,W,C), col (R*H*W, 9*C); col2im is its adjoint (dx = sum over the
+ * 9 taps, in (kh,kw) order).  C % 4 == 0, 16-B aligned. */
+int tlod_im2col3x3_nhwc_f32(const float* x, int R, int H, int W, int C, float* col,
+                            tlod_stream_t stream);
+int tlod_col2im3x3_nhwc_f32(const float* col, int R, int H, int W, int C, float* dx,
+                            tlod_stream_t stream);
 
 
 /* ------------------------------------------------------------------ Optimiser step

@@ -213,3 +213,24 @@ def test_daf_resnet101_proposals_without_override():
         assert abs(gv - r) <= 1e-4 * max(abs(r), 1e-3), (name, gv, r)
     for key, ref_key in (("s_rois", "props"), ("t_rois", "t_props")):
         assert_proposal_sets_match(m.capture[key].cpu().numpy(), ref[ref_key], key)
+
+
+@pytest.mark.parametrize("R,H,W,C", [(5, 4, 4, 32), (3, 2, 7, 512), (2, 1, 1, 4)])
+def test_im2col3x3_nhwc(R, H, W, C):
+    """tlod_im2col3x3_nhwc_f32 / col2im (the RoI head's 3x3 convs) against the torch
+    composition they replace (F.pad + 9 slices + cat): forward bit-exact, backward to fp32
+    summation order."""
+    import torch.nn.functional as F
+    from tlod.detector.resnet import Im2col3x3Function
+    g = torch.Generator().manual_seed(R * 100 + C)
+    x = torch.randn(R, H, W, C, generator=g).to(dev).requires_grad_(True)
+    col = Im2col3x3Function.apply(x)
+    xr = x.detach().clone().requires_grad_(True)
+    pad = F.pad(xr, (0, 0, 1, 1, 1, 1))
+    ref = torch.cat([pad[:, kh:kh + H, kw:kw + W, :] for kh in range(3) for kw in range(3)],
+                    3).reshape(R * H * W, 9 * C)
+    assert torch.equal(col, ref)
+    gy = torch.randn(R * H * W, 9 * C, generator=g).to(dev)
+    col.backward(gy)
+    ref.backward(gy)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-6, atol=1e-6)

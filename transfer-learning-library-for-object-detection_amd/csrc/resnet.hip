@@ -114,6 +114,51 @@ static unsigned grid_for(size_t total) {
   return (unsigned)std::min<size_t>((total + 255) / 256, 16384);
 }
 
+// RoI head 3x3 convs (layer4 on R x 4 x 4 maps, channels-last) as GEMMs over a 9-tap
+// gather: col[(r,h,w)][(kh,kw,c)] = x[r][h+kh-1][w+kw-1][c] (zero outside the map), one
+// thread per (row, 4 channels), 9 16-B loads and stores; the adjoint sums the 9 taps of each
+// input element in (kh, kw) order (a gather: no atomics, deterministic).  Replaces F.pad +
+// 9 slices + torch.cat (and their backward: 9 zero-filled slice gradients summed by autograd).
+__global__ void im2col3x3_nhwc_kernel(const float4* __restrict__ x, int H, int W, int C4,
+                                      size_t total, float4* __restrict__ col) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4);
+    const size_t row = i / C4;
+    const int w = (int)(row % W), h = (int)((row / W) % H);
+    const size_t r = row / ((size_t)H * W);
+    float4* o = col + row * 9 * C4 + c;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = h + t / 3 - 1, ww = w + t % 3 - 1;
+      o[(size_t)t * C4] = (hh >= 0 && hh < H && ww >= 0 && ww < W)
+                              ? x[((r * H + hh) * W + ww) * C4 + c]
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+__global__ void col2im3x3_nhwc_kernel(const float4* __restrict__ col, int H, int W, int C4,
+                                      size_t total, float4* __restrict__ dx) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4);
+    const size_t row = i / C4;
+    const int w = (int)(row % W), h = (int)((row / W) % H);
+    const size_t r = row / ((size_t)H * W);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {  // output pixel (h - kh + 1, w - kw + 1) took x(h, w) as tap t
+      const int oh = h - t / 3 + 1, ow = w - t % 3 + 1;
+      if (oh >= 0 && oh < H && ow >= 0 && ow < W) {
+        const float4 v = col[(((r * H + oh) * W + ow) * 9 + t) * C4 + c];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+    }
+    dx[i] = a;
+  }
+}
+
 }  // namespace tlod
 
 using namespace tlod;
@@ -136,6 +181,32 @@ extern "C" int tlod_upsample2_zero_f32(const float* dy, int N, int C, int H, int
   const size_t total = (size_t)N * C * H * W;
   hipLaunchKernelGGL(upsample2_zero_kernel, dim3(grid_for(total)), dim3(256), 0,
                      (hipStream_t)stream, dy, H, W, Ho, Wo, total, dx);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_im2col3x3_nhwc_f32(const float* x, int R, int H, int W, int C, float* col,
+                                      tlod_stream_t stream) {
+  TLOD_CHECK_ARG(R > 0 && H > 0 && W > 0 && C > 0 && (C & 3) == 0 && x && col, "bad arguments");
+  TLOD_CHECK_ARG(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(col)) & 15) == 0,
+                 "16-B aligned tensors");
+  const size_t total = (size_t)R * H * W * (C / 4);
+  hipLaunchKernelGGL(im2col3x3_nhwc_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, reinterpret_cast<const float4*>(x), H, W, C / 4, total,
+                     reinterpret_cast<float4*>(col));
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_col2im3x3_nhwc_f32(const float* col, int R, int H, int W, int C, float* dx,
+                                      tlod_stream_t stream) {
+  TLOD_CHECK_ARG(R > 0 && H > 0 && W > 0 && C > 0 && (C & 3) == 0 && col && dx, "bad arguments");
+  TLOD_CHECK_ARG(((reinterpret_cast<uintptr_t>(col) | reinterpret_cast<uintptr_t>(dx)) & 15) == 0,
+                 "16-B aligned tensors");
+  const size_t total = (size_t)R * H * W * (C / 4);
+  hipLaunchKernelGGL(col2im3x3_nhwc_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, reinterpret_cast<const float4*>(col), H, W, C / 4, total,
+                     reinterpret_cast<float4*>(dx));
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

@@ -121,6 +121,8 @@ SIGNATURES = {
     "tlod_stem_conv7x7s2_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_im2col3x3_nhwc_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_col2im3x3_nhwc_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_image_blob_u8": (c_int, [P, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_int, P, P]),
     "tlod_detect_f32": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_float, c_float, c_float,

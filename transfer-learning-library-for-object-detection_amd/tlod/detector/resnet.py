@@ -13,8 +13,9 @@ in eval mode (:249-284).  Execution:
     conv1 and the downsample share the subsampled tensor);
   * the stem (7x7/2 conv + bn1 + ReLU, frozen) is tlod_stem_conv7x7s2_f32;
   * the RoI head (layer4 on R x 1024 x 7x7 -> 4x4 maps) runs channels-last: 1x1 convs
-    are plain GEMMs and the 3x3 convs GEMMs over a 9-tap gather (hipBLASLt through
-    torch.matmul) — 4x4 maps would fill 16 of the 256 pixel slots of a conv tile.
+    are plain GEMMs and the 3x3 convs GEMMs over a 9-tap gather, on libtlod's split-bf16
+    GEMM (tlod.linear; TLOD_LINEAR_MATH=f32: hipBLASLt through torch.addmm) — 4x4 maps
+    would fill 16 of the 256 pixel slots of a conv tile.
 """
 import math
 
@@ -24,6 +25,7 @@ import torch.nn.functional as F
 
 from .. import _lib
 from ..conv import ConvBNFunction
+from ..linear import LinearFunction, linear_math
 
 
 def fold_bn(bn):
@@ -64,6 +66,40 @@ class Subsample2Function(torch.autograd.Function):
         _lib.check(_lib.lib().tlod_upsample2_zero_f32(_lib.ptr(g), N, C, H, W, _lib.ptr(dx),
                                                       _lib.stream_of(g)), "upsample2_zero")
         return dx
+
+
+class Im2col3x3Function(torch.autograd.Function):
+    """x (R,H,W,C) channels-last -> (R*H*W, 9*C) taps in (kh, kw, c) order, zero padding 1
+    (tlod_im2col3x3_nhwc_f32; backward tlod_col2im3x3_nhwc_f32)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _lib.require_cuda(x)
+        x = x.contiguous()
+        R, H, W, C = x.shape
+        col = torch.empty((R * H * W, 9 * C), dtype=x.dtype, device=x.device)
+        _lib.check(_lib.lib().tlod_im2col3x3_nhwc_f32(_lib.ptr(x), R, H, W, C, _lib.ptr(col),
+                                                      _lib.stream_of(x)), "im2col3x3_nhwc")
+        ctx.shape = (R, H, W, C)
+        return col
+
+    @staticmethod
+    def backward(ctx, g):
+        R, H, W, C = ctx.shape
+        g = g.contiguous()
+        dx = torch.empty((R, H, W, C), dtype=g.dtype, device=g.device)
+        _lib.check(_lib.lib().tlod_col2im3x3_nhwc_f32(_lib.ptr(g), R, H, W, C, _lib.ptr(dx),
+                                                      _lib.stream_of(g)), "col2im3x3_nhwc")
+        return dx
+
+
+def im2col3x3_nhwc(x):
+    if x.shape[3] % 4 == 0:
+        return Im2col3x3Function.apply(x)
+    R, H, W, P = x.shape  # (unaligned channel counts: the torch composition)
+    pad = F.pad(x, (0, 0, 1, 1, 1, 1))
+    return torch.cat([pad[:, kh:kh + H, kw:kw + W, :] for kh in range(3) for kw in range(3)],
+                     3).reshape(R * H * W, 9 * P)
 
 
 def conv_bn(x, conv, bn, relu, residual=None):
@@ -124,8 +160,13 @@ class Bottleneck(nn.Module):
         w = conv.weight
         wm = w.view(w.shape[0], -1) if w.shape[2] == 1 else w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
         # BN scale folded into the (small) weight, shift as the GEMM's bias: one GEMM with
-        # its bias epilogue instead of GEMM + two passes over the (R*H*W, C) output
-        y = torch.addmm(shift, xm, (wm * scale[:, None]).t())
+        # its bias epilogue instead of GEMM + two passes over the (R*H*W, C) output; the
+        # GEMMs (forward, input and weight gradient) on libtlod's split-bf16 GEMM
+        m = linear_math()
+        if m == "f32":
+            y = torch.addmm(shift, xm, (wm * scale[:, None]).t())
+        else:
+            y = LinearFunction.apply(xm.contiguous(), wm * scale[:, None], shift, m)
         if residual is not None:
             y = y.add_(residual)
         return F.relu(y, inplace=True) if relu else y
@@ -139,9 +180,8 @@ class Bottleneck(nn.Module):
         out = self._gemm_bn(xm, self.conv1, self.bn1, relu=True)
         P = out.shape[1]
         self._tap("r1", out.view(R, H, W, P), nhwc=True)
-        pad = F.pad(out.view(R, H, W, P), (0, 0, 1, 1, 1, 1))
-        taps = torch.cat([pad[:, kh:kh + H, kw:kw + W, :] for kh in range(3) for kw in range(3)], 3)
-        out = self._gemm_bn(taps.reshape(R * H * W, 9 * P), self.conv2, self.bn2, relu=True)
+        taps = im2col3x3_nhwc(out.view(R, H, W, P))
+        out = self._gemm_bn(taps, self.conv2, self.bn2, relu=True)
         self._tap("r2", out.view(R, H, W, P), nhwc=True)
         res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False)
                if self.downsample is not None else xm)
