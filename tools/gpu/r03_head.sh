@@ -13,7 +13,7 @@ for r in 1 2; do
     for cfg in "daf res101" "atf res101"; do
       set -- $cfg
       TLOD_LINEAR_MATH=$m timeout -k 10 400 python3 bench.py --method $1 --net $2 --steps 6 --warmup 2 --cpu-baseline-steps 0 > $O/b_${1}_${m}_${r}.json 2> $O/b_${1}_${m}_${r}.err
-      echo "$m $cfg r$r: $(python3 -c "import json;d=json.load(open("$O/b_${1}_${m}_${r}.json"));print(d['value'], d['ms_per_step'])")"
+      echo "$m $cfg r$r: $(python3 -c "import json;d=json.load(open('$O/b_${1}_${m}_${r}.json'));print(d['value'], d['ms_per_step'])")"
     done
   done
 done
