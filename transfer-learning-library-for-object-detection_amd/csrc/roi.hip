@@ -483,13 +483,32 @@ __global__ void __launch_bounds__(256) rbg_seg_fixup_kernel(
   const int n = start[ncell];
   if (seg * 64 >= n || !(flags[seg] & 1)) return;
   const int c = blockIdx.y * 64 + lane;
-  if (c >= C) return;
   const unsigned cell = keys[min(seg * 64 + 64, n) - 1];
-  float a = carry_tail[(size_t)seg * C + c];
-  for (int k = seg + 1; k * 64 < n; ++k) {
-    a += carry_head[(size_t)k * C + c];
-    if (!(flags[k] & 2)) break;
+  // the run ends in the first later segment not flagged 2: found 64 flags at a time by the
+  // lanes (a cell under hundreds of RoIs spans hundreds of segments), then its head pieces
+  // summed in order with the loads batched
+  int kend = seg + 1;
+  for (int kb = seg + 1;; kb += 64) {
+    const int k = kb + lane;
+    const bool stop = k * 64 >= n || !(flags[k] & 2);
+    const unsigned long long m = __ballot(stop);
+    if (m) {
+      kend = kb + __builtin_ctzll(m);
+      break;
+    }
   }
+  if (kend * 64 >= n) --kend;
+  if (c >= C) return;
+  float a = carry_tail[(size_t)seg * C + c];
+  int k = seg + 1;
+  for (; k + 8 <= kend + 1; k += 8) {
+    float h[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) h[u] = carry_head[(size_t)(k + u) * C + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += h[u];
+  }
+  for (; k <= kend; ++k) a += carry_head[(size_t)k * C + c];
   acc[(size_t)cell * C + c] = a;
 }
 
