@@ -421,7 +421,10 @@ class ConvBNFunction(torch.autograd.Function):
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.wparam = weight
+        ctx.mask_in = _relu_out(x)
         ctx.save_for_backward(x, weight, scale, y if relu else None)
+        if relu:
+            y._tlod_relu_out = True
         return y
 
     @staticmethod
@@ -429,8 +432,22 @@ class ConvBNFunction(torch.autograd.Function):
         x, weight, scale, y = ctx.saved_tensors
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_res = ctx.has_res and ctx.needs_input_grad[4]
+        mask = x if ctx.mask_in else None
+        if (ctx.relu and y is not None and
+                getattr(dy, "_tlod_relu_masked", None) == (y.data_ptr(), dy.data_ptr(), dy._version)):
+            # dy is the next conv's dgrad, already masked by this ReLU (a bottleneck's 3x3 conv2
+            # masks conv1's gradient): the BN scale g = dy * scale folds into the dgrad weight
+            # (W * scale per output channel) and the weight gradient's rows — no pass over dy
+            STATS["relu_bwd_skipped"] += 1
+            s4 = scale.detach().view(-1, 1, 1, 1)
+            dx = conv_dgrad(dy, weight.detach() * s4, mask=mask) if need_x else None
+            dw = None
+            if need_w:
+                dw = conv_wgrad(dy, x, weight.shape[2], out=grad_out(ctx.wparam))
+                dw.mul_(s4)
+            return dx, dw, None, None, dy if need_res else None, None
         g, g_raw = relu_bwd_ex(dy, y if ctx.relu else None, scale, want_raw=need_res)
-        dx = conv_dgrad(g, weight) if need_x else None
+        dx = conv_dgrad(g, weight, mask=mask) if need_x else None
         dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.wparam)) if need_w else None
         return dx, dw, None, None, g_raw, None
 
