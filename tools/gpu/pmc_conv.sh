@@ -1,5 +1,5 @@
-# Round-3 lease: clock / MFMA-busy / LDS counters of the warp-specialized conv (conv3_3
-# shapes) and the wgrad kernel.  usage: bash tools/gpu/r03_pmc_ws.sh OUTDIR
+# Clock / MFMA-busy / LDS counters of the warp-specialized conv (conv3_3
+# shapes) and the wgrad kernel.  usage: bash tools/gpu/pmc_conv.sh OUTDIR
 set -e
 O=$1
 mkdir -p $O

@@ -1,5 +1,5 @@
-# Round-3 end: full GPU test suite, smoke, then the round profile (tools/gpu/profile.sh).
-# usage: bash tools/gpu/r03_final.sh OUTDIR
+# Round end: full GPU test suite, smoke, then the round profile (tools/gpu/profile.sh).
+# usage: bash tools/gpu/round_end.sh OUTDIR
 set -e
 cd "$GRAFT_REPO_ROOT"
 O=$1
