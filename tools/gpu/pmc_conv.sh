@@ -12,9 +12,3 @@ python3 tools/pmc_kernel.py $O/p1 > $O/p1.txt
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU --output-format csv -d $O/p2 -o run -- $C > $O/p2.out 2> $O/p2.err
 python3 tools/pmc_kernel.py $O/p2 > $O/p2.txt
 cat $O/p1.txt $O/p2.txt
-timeout -k 10 600 python -u -m pytest tests/test_resnet_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest_resnet.log 2>&1
-tail -2 $O/pytest_resnet.log
-for r in 1 2; do
-  timeout -k 10 300 python3 bench.py --net res101 --steps 10 --warmup 3 --cpu-baseline-steps 0 > $O/r101_$r.json 2> $O/r101_$r.err
-  python3 -c "import json;d=json.load(open('$O/r101_$r.json'));print('r101', d['value'], d['ms_per_step'])"
-done
