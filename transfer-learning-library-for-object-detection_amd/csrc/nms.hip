@@ -67,6 +67,9 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
   }
 }
 
+#ifndef TLOD_NMS_TRI
+#define TLOD_NMS_TRI 1
+#endif
 constexpr int kScanThreads = 1024;
 constexpr int kMaxColBlocks = 2048;  // n <= 131072
 constexpr int kFastColBlocks = 256;  // n <= 16384: the pipelined scan below
@@ -97,12 +100,17 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
   // 32-bit byte offsets from the uniform base (n * col_blocks * 8 <= 32 MiB): one VGPR
   // per address, so the three buffers fit the 128-VGPR budget of a 1024-thread group
   const char* mbase = reinterpret_cast<const char*>(mask);
+  // Only the words right of the diagonal block are ever used (column c > b for the rows of
+  // block b): the lanes of columns <= b all read column b + 1's word instead (one cache line
+  // per row, results unused), so the scan fetches the mask's upper triangle only
+  // (TLOD_NMS_TRI=0: every column).
   auto load_rows = [&](int b, unsigned long long (&r)[16], unsigned long long& d) {
+    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= b ? min(b + 1, col_blocks - 1) : cc);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const unsigned row = (unsigned)min(b * 64 + g * 16 + j, n - 1);
       r[j] = *reinterpret_cast<const unsigned long long*>(
-          mbase + (row * (unsigned)col_blocks + (unsigned)cc) * 8u);
+          mbase + (row * (unsigned)col_blocks + col) * 8u);
     }
     if (t < 64) d = diag_t[min(b, col_blocks - 1) * 64 + t];
   };
