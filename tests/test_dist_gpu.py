@@ -152,3 +152,45 @@ def test_fused_sgd_partial_gradients_two_ranks(tmp_path):
     assert not torch.equal(r0["w"]["head2.weight"], r0["w0"]["head2.weight"])
     assert torch.equal(r0["w"]["unused.weight"], r0["w0"]["unused.weight"])
     assert torch.equal(r0["w"]["unused.bias"], r0["w0"]["unused.bias"])
+
+
+def _worker_cfg(rank, world, port, outdir, method, net):
+    """BASELINE configs 3 and 5 (8-GPU DAF-R101 / ATF-R101) on two ranks: one step each."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    from tlod.detector.train import build_model, make_optimizer, train_step
+    from tlod.dist import GradBucketReducer
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = build_model(method, dev, net, seed=rank)  # rank 1's init is overwritten by rank 0's
+    opt = make_optimizer(m, 2e-3, clip=10.0)
+    red = GradBucketReducer(m, bucket_mb=16.0)
+    w0 = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    loss = train_step(m, opt, _batch(rank, 0, dev), reducer=red)
+    torch.cuda.synchronize()
+    torch.save({"w0": w0, "loss": float(loss),
+                "w": {k: v.detach().cpu().clone() for k, v in m.named_parameters()}},
+               os.path.join(outdir, f"{method}{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("method,net", [("daf", "res101"), ("atf", "res101")])
+def test_resnet101_configs_data_parallel_two_ranks(tmp_path, method, net):
+    """Configs 3 / 5 run data-parallel: after one step on different images the two ranks'
+    weights are bit-identical (the broadcast initial weights, the SUM all-reduce over the
+    arena, the same fused update), finite, and moved."""
+    port = _free_port()
+    mp.spawn(_worker_cfg, args=(2, port, str(tmp_path), method, net), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / f"{method}0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / f"{method}1.pt", weights_only=True)
+    moved = 0
+    for k in r0["w"]:
+        assert torch.equal(r0["w"][k], r1["w"][k]), k
+        assert torch.isfinite(r0["w"][k]).all(), k
+        moved += int(not torch.equal(r0["w"][k], r0["w0"][k]))
+    assert moved > 0
+    assert r0["loss"] == r0["loss"] and r1["loss"] == r1["loss"]  # not NaN
