@@ -87,43 +87,51 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
     int n, int col_blocks, int max_keep, int32_t* __restrict__ keep,
     int32_t* __restrict__ num_keep) {
   __shared__ unsigned long long remv[kFastColBlocks];
-  __shared__ unsigned long long s_kept;
+  __shared__ unsigned long long s_kept[2];
   __shared__ int s_total, s_done;
   const int t = threadIdx.x;
   const int c = t & 255, g = t >> 8;
   const int cc = min(c, col_blocks - 1);  // clamped column (masked later)
   if (t < kFastColBlocks) remv[t] = 0ull;
-  if (t == 0) { s_total = 0; s_done = 0; s_kept = 0ull; }
+  if (t == 0) { s_total = 0; s_done = 0; s_kept[0] = s_kept[1] = 0ull; }
 
+  // Iteration b: wave 0 resolves block b while the other waves OR block b-1's survivors into
+  // the columns >= b+1 — one barrier per block.  Column b+1 of block b's survivors (what
+  // block b+1 needs next) wave 0 adds itself right after resolving b, from its own copy of
+  // those 64 words.  Register set of iteration it (loaded two iterations ahead): rows of
+  // block it-1 (all threads), block it's diagonal words and its column-(it+1) words (wave 0).
   unsigned long long r0[16], r1[16], r2[16];
-  unsigned long long d0 = 0ull, d1 = 0ull, d2 = 0ull;
+  unsigned long long d0 = 0ull, d1 = 0ull, d2 = 0ull, w0 = 0ull, w1 = 0ull, w2 = 0ull;
   // 32-bit byte offsets from the uniform base (n * col_blocks * 8 <= 32 MiB): one VGPR
   // per address, so the three buffers fit the 128-VGPR budget of a 1024-thread group
   const char* mbase = reinterpret_cast<const char*>(mask);
-  // Only the words right of the diagonal block are ever used (column c > b for the rows of
-  // block b): the lanes of columns <= b all read column b + 1's word instead (one cache line
-  // per row, results unused), so the scan fetches the mask's upper triangle only
-  // (TLOD_NMS_TRI=0: every column).
-  auto load_rows = [&](int b, unsigned long long (&r)[16], unsigned long long& d) {
-    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= b ? min(b + 1, col_blocks - 1) : cc);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const unsigned row = (unsigned)min(b * 64 + g * 16 + j, n - 1);
-      r[j] = *reinterpret_cast<const unsigned long long*>(
-          mbase + (row * (unsigned)col_blocks + col) * 8u);
-    }
-    if (t < 64) d = diag_t[min(b, col_blocks - 1) * 64 + t];
+  auto word = [&](unsigned row, unsigned col) {
+    return *reinterpret_cast<const unsigned long long*>(mbase + (row * (unsigned)col_blocks + col) * 8u);
   };
-  load_rows(0, r0, d0);
-  load_rows(min(1, col_blocks - 1), r1, d1);
+  auto load_set = [&](int it, unsigned long long (&r)[16], unsigned long long& d,
+                      unsigned long long& w) {
+    // only columns > it of block it-1's rows are used: lanes of columns <= it all read one
+    // word (the mask's upper triangle is what the scan fetches; TLOD_NMS_TRI=0: all)
+    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= it ? min(it + 1, col_blocks - 1) : cc);
+    const int pb = max(it - 1, 0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) r[j] = word((unsigned)min(pb * 64 + g * 16 + j, n - 1), col);
+    if (t < 64) {
+      const int bb = min(it, col_blocks - 1);
+      d = diag_t[bb * 64 + t];
+      w = word((unsigned)min(bb * 64 + t, n - 1), (unsigned)min(bb + 1, col_blocks - 1));
+    }
+  };
+  load_set(0, r0, d0, w0);
+  load_set(1, r1, d1, w1);
   __syncthreads();
 
-  // One block of the scan; `cur` holds block b's rows, `ahead` receives block b+2's.
-  // Unrolled x3 below so the three register buffers never move (a copy of a register
-  // with a load in flight would wait for that load).
+  // Unrolled x3 below so the three register sets never move (a copy of a register with a
+  // load in flight would wait for that load).
   auto step = [&](int b, const unsigned long long (&cur)[16], unsigned long long dcur,
-                  unsigned long long (&ahead)[16], unsigned long long& dahead) -> bool {
-    load_rows(min(b + 2, col_blocks - 1), ahead, dahead);
+                  unsigned long long wcur, unsigned long long (&ahead)[16],
+                  unsigned long long& dahead, unsigned long long& wahead) -> bool {
+    load_set(b + 2, ahead, dahead, wahead);
     if (t < 64) {  // wave 0: resolve block b
       const int valid = min(n - b * 64, 64);
       const unsigned long long vmask = valid == 64 ? ~0ull : ((1ull << valid) - 1ull);
@@ -146,31 +154,33 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
         kept = k2;
         kc = room;
       }
-      if ((kept >> t) & 1ull)
+      if ((kept >> t) & 1ull) {
         keep[total + __popcll(kept & ((1ull << t) - 1ull))] = b * 64 + t;
+        if (b + 1 < col_blocks && wcur) atomicOr(&remv[b + 1], wcur);  // near column
+      }
       if (t == 0) {
-        s_kept = kept;
+        s_kept[b & 1] = kept;
         s_total = total + kc;
         if (max_keep > 0 && total + kc >= max_keep) s_done = 1;
       }
     }
-    __syncthreads();
-    if (s_done) return true;
-    const unsigned long long kept = s_kept;
-    const unsigned kg = (unsigned)(kept >> (g * 16)) & 0xffffu;
-    if (kg && c > b && c < col_blocks) {
-      unsigned long long v = 0ull;
+    if (b >= 1) {  // block b-1's survivors into the columns >= b+1
+      const unsigned long long kp = s_kept[(b - 1) & 1];
+      const unsigned kg = (unsigned)(kp >> (g * 16)) & 0xffffu;
+      if (kg && c > b && c < col_blocks) {
+        unsigned long long v = 0ull;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v |= ((kg >> j) & 1u) ? cur[j] : 0ull;
-      if (v) atomicOr(&remv[c], v);
+        for (int j = 0; j < 16; ++j) v |= ((kg >> j) & 1u) ? cur[j] : 0ull;
+        if (v) atomicOr(&remv[c], v);
+      }
     }
     __syncthreads();
-    return false;
+    return s_done != 0;
   };
   for (int b = 0; b < col_blocks; b += 3) {
-    if (step(b, r0, d0, r2, d2) || b + 1 >= col_blocks) break;
-    if (step(b + 1, r1, d1, r0, d0) || b + 2 >= col_blocks) break;
-    if (step(b + 2, r2, d2, r1, d1)) break;
+    if (step(b, r0, d0, w0, r2, d2, w2) || b + 1 >= col_blocks) break;
+    if (step(b + 1, r1, d1, w1, r0, d0, w0) || b + 2 >= col_blocks) break;
+    if (step(b + 2, r2, d2, w2, r1, d1, w1)) break;
   }
   if (t == 0) *num_keep = s_total;
 }
