@@ -87,51 +87,62 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
     int n, int col_blocks, int max_keep, int32_t* __restrict__ keep,
     int32_t* __restrict__ num_keep) {
   __shared__ unsigned long long remv[kFastColBlocks];
-  __shared__ unsigned long long s_kept[2];
+  __shared__ unsigned long long s_kept[4];
   __shared__ int s_total, s_done;
   const int t = threadIdx.x;
   const int c = t & 255, g = t >> 8;
   const int cc = min(c, col_blocks - 1);  // clamped column (masked later)
   if (t < kFastColBlocks) remv[t] = 0ull;
-  if (t == 0) { s_total = 0; s_done = 0; s_kept[0] = s_kept[1] = 0ull; }
+  if (t < 4) s_kept[t] = 0ull;
+  if (t == 0) { s_total = 0; s_done = 0; }
 
-  // Iteration b: wave 0 resolves block b while the other waves OR block b-1's survivors into
-  // the columns >= b+1 — one barrier per block.  Column b+1 of block b's survivors (what
-  // block b+1 needs next) wave 0 adds itself right after resolving b, from its own copy of
-  // those 64 words.  Register set of iteration it (loaded two iterations ahead): rows of
-  // block it-1 (all threads), block it's diagonal words and its column-(it+1) words (wave 0).
-  unsigned long long r0[16], r1[16], r2[16];
-  unsigned long long d0 = 0ull, d1 = 0ull, d2 = 0ull, w0 = 0ull, w1 = 0ull, w2 = 0ull;
+  // Iteration b: wave 0 resolves block b, then ORs its survivors' words of columns b+1..b+3
+  // into remv itself (from 3 words per lane it prefetched: the near columns); meanwhile
+  // every thread fetches the rows of block b-1's SURVIVORS only (about one row in six) and
+  // ORs block b-3's survivors, fetched two iterations ago, into the columns beyond b.  One
+  // barrier per block, and the mask rows of suppressed boxes are never read.  Thread
+  // (g, c) owns column c of rows g*16..g*16+15 of a block; a wave's rows are one g, so the
+  // survivor test per row is wave-uniform.
+  unsigned long long r0[16], r1[16], r2[16];  // survivor rows, ring by block % 3
+  unsigned long long d0 = 0ull, d1 = 0ull, d2 = 0ull;  // wave 0: block's diagonal words
+  unsigned long long n0[3] = {0ull, 0ull, 0ull}, n1[3] = {0ull, 0ull, 0ull},
+                     n2[3] = {0ull, 0ull, 0ull};  // wave 0: near columns
   // 32-bit byte offsets from the uniform base (n * col_blocks * 8 <= 32 MiB): one VGPR
-  // per address, so the three buffers fit the 128-VGPR budget of a 1024-thread group
+  // per address
   const char* mbase = reinterpret_cast<const char*>(mask);
   auto word = [&](unsigned row, unsigned col) {
     return *reinterpret_cast<const unsigned long long*>(mbase + (row * (unsigned)col_blocks + col) * 8u);
   };
-  auto load_set = [&](int it, unsigned long long (&r)[16], unsigned long long& d,
-                      unsigned long long& w) {
-    // only columns > it of block it-1's rows are used: lanes of columns <= it all read one
-    // word (the mask's upper triangle is what the scan fetches; TLOD_NMS_TRI=0: all)
-    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= it ? min(it + 1, col_blocks - 1) : cc);
-    const int pb = max(it - 1, 0);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) r[j] = word((unsigned)min(pb * 64 + g * 16 + j, n - 1), col);
+  // wave 0's words of block bb: diagonal, and columns bb+1..bb+3 of its 64 rows
+  auto load_w0 = [&](int bb, unsigned long long& d, unsigned long long (&nw)[3]) {
     if (t < 64) {
-      const int bb = min(it, col_blocks - 1);
-      d = diag_t[bb * 64 + t];
-      w = word((unsigned)min(bb * 64 + t, n - 1), (unsigned)min(bb + 1, col_blocks - 1));
+      const int b1 = min(bb, col_blocks - 1);
+      d = diag_t[b1 * 64 + t];
+      const unsigned row = (unsigned)min(b1 * 64 + t, n - 1);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) nw[q] = word(row, (unsigned)min(b1 + 1 + q, col_blocks - 1));
     }
   };
-  load_set(0, r0, d0, w0);
-  load_set(1, r1, d1, w1);
+  // rows of block p's survivors (kept mask kp), the columns > p + 3 they are used for
+  auto load_rows = [&](int p, unsigned long long kp, unsigned long long (&r)[16]) {
+    const unsigned kg = (unsigned)(kp >> (g * 16)) & 0xffffu;
+    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= p + 3 ? min(p + 4, col_blocks - 1) : cc);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((kg >> j) & 1u) r[j] = word((unsigned)(p * 64 + g * 16 + j), col);
+  };
+  load_w0(0, d0, n0);
+  load_w0(1, d1, n1);
   __syncthreads();
 
-  // Unrolled x3 below so the three register sets never move (a copy of a register with a
-  // load in flight would wait for that load).
-  auto step = [&](int b, const unsigned long long (&cur)[16], unsigned long long dcur,
-                  unsigned long long wcur, unsigned long long (&ahead)[16],
-                  unsigned long long& dahead, unsigned long long& wahead) -> bool {
-    load_set(b + 2, ahead, dahead, wahead);
+  // Unrolled x3 below so the register sets never move (a copy of a register with a load
+  // in flight would wait for that load): iteration b loads rows of block b-1 into set
+  // (b-1) % 3 and uses set b % 3 (block b-3's rows).
+  auto step = [&](int b, unsigned long long dcur, const unsigned long long (&ncur)[3],
+                  unsigned long long& dnext, unsigned long long (&nnext)[3],
+                  unsigned long long (&rload)[16], const unsigned long long (&ruse)[16]) -> bool {
+    if (b >= 1) load_rows(b - 1, s_kept[(b - 1) & 3], rload);
+    load_w0(b + 2, dnext, nnext);
     if (t < 64) {  // wave 0: resolve block b
       const int valid = min(n - b * 64, 64);
       const unsigned long long vmask = valid == 64 ? ~0ull : ((1ull << valid) - 1ull);
@@ -156,21 +167,22 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
       }
       if ((kept >> t) & 1ull) {
         keep[total + __popcll(kept & ((1ull << t) - 1ull))] = b * 64 + t;
-        if (b + 1 < col_blocks && wcur) atomicOr(&remv[b + 1], wcur);  // near column
+#pragma unroll
+        for (int q = 0; q < 3; ++q)  // near columns b+1..b+3
+          if (b + 1 + q < col_blocks && ncur[q]) atomicOr(&remv[b + 1 + q], ncur[q]);
       }
       if (t == 0) {
-        s_kept[b & 1] = kept;
+        s_kept[b & 3] = kept;
         s_total = total + kc;
         if (max_keep > 0 && total + kc >= max_keep) s_done = 1;
       }
     }
-    if (b >= 1) {  // block b-1's survivors into the columns >= b+1
-      const unsigned long long kp = s_kept[(b - 1) & 1];
-      const unsigned kg = (unsigned)(kp >> (g * 16)) & 0xffffu;
+    if (b >= 3) {  // block b-3's survivors into the columns beyond b
+      const unsigned kg = (unsigned)(s_kept[(b - 3) & 3] >> (g * 16)) & 0xffffu;
       if (kg && c > b && c < col_blocks) {
         unsigned long long v = 0ull;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v |= ((kg >> j) & 1u) ? cur[j] : 0ull;
+        for (int j = 0; j < 16; ++j) v |= ((kg >> j) & 1u) ? ruse[j] : 0ull;
         if (v) atomicOr(&remv[c], v);
       }
     }
@@ -178,9 +190,9 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
     return s_done != 0;
   };
   for (int b = 0; b < col_blocks; b += 3) {
-    if (step(b, r0, d0, w0, r2, d2, w2) || b + 1 >= col_blocks) break;
-    if (step(b + 1, r1, d1, w1, r0, d0, w0) || b + 2 >= col_blocks) break;
-    if (step(b + 2, r2, d2, w2, r1, d1, w1)) break;
+    if (step(b, d0, n0, d2, n2, r2, r0) || b + 1 >= col_blocks) break;
+    if (step(b + 1, d1, n1, d0, n0, r0, r1) || b + 2 >= col_blocks) break;
+    if (step(b + 2, d2, n2, d1, n1, r1, r2)) break;
   }
   if (t == 0) *num_keep = s_total;
 }
