@@ -96,53 +96,51 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
   if (t < 4) s_kept[t] = 0ull;
   if (t == 0) { s_total = 0; s_done = 0; }
 
-  // Iteration b: wave 0 resolves block b, then ORs its survivors' words of columns b+1..b+3
-  // into remv itself (from 3 words per lane it prefetched: the near columns); meanwhile
+  // Iteration b: wave 0 resolves block b, then ORs its survivors' words of columns b+1, b+2
+  // into remv itself (from 2 words per lane it prefetched: the near columns); meanwhile
   // every thread fetches the rows of block b-1's SURVIVORS only (about one row in six) and
-  // ORs block b-3's survivors, fetched two iterations ago, into the columns beyond b.  One
+  // ORs block b-2's survivors, fetched in the previous iteration, into the columns beyond b.  One
   // barrier per block, and the mask rows of suppressed boxes are never read.  Thread
   // (g, c) owns column c of rows g*16..g*16+15 of a block; a wave's rows are one g, so the
   // survivor test per row is wave-uniform.
-  unsigned long long r0[16], r1[16], r2[16];  // survivor rows, ring by block % 3
-  unsigned long long d0 = 0ull, d1 = 0ull, d2 = 0ull;  // wave 0: block's diagonal words
-  unsigned long long n0[3] = {0ull, 0ull, 0ull}, n1[3] = {0ull, 0ull, 0ull},
-                     n2[3] = {0ull, 0ull, 0ull};  // wave 0: near columns
+  unsigned long long r0[16], r1[16];  // survivor rows, by block % 2
+  unsigned long long d0 = 0ull, d1 = 0ull;  // wave 0: block's diagonal words
+  unsigned long long n0[2] = {0ull, 0ull}, n1[2] = {0ull, 0ull};  // wave 0: near columns
   // 32-bit byte offsets from the uniform base (n * col_blocks * 8 <= 32 MiB): one VGPR
   // per address
   const char* mbase = reinterpret_cast<const char*>(mask);
   auto word = [&](unsigned row, unsigned col) {
     return *reinterpret_cast<const unsigned long long*>(mbase + (row * (unsigned)col_blocks + col) * 8u);
   };
-  // wave 0's words of block bb: diagonal, and columns bb+1..bb+3 of its 64 rows
-  auto load_w0 = [&](int bb, unsigned long long& d, unsigned long long (&nw)[3]) {
+  // wave 0's words of block bb: diagonal, and columns bb+1, bb+2 of its 64 rows
+  auto load_w0 = [&](int bb, unsigned long long& d, unsigned long long (&nw)[2]) {
     if (t < 64) {
       const int b1 = min(bb, col_blocks - 1);
       d = diag_t[b1 * 64 + t];
       const unsigned row = (unsigned)min(b1 * 64 + t, n - 1);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) nw[q] = word(row, (unsigned)min(b1 + 1 + q, col_blocks - 1));
+      for (int q = 0; q < 2; ++q) nw[q] = word(row, (unsigned)min(b1 + 1 + q, col_blocks - 1));
     }
   };
-  // rows of block p's survivors (kept mask kp), the columns > p + 3 they are used for
+  // rows of block p's survivors (kept mask kp), the columns > p + 2 they are used for
   auto load_rows = [&](int p, unsigned long long kp, unsigned long long (&r)[16]) {
     const unsigned kg = (unsigned)(kp >> (g * 16)) & 0xffffu;
-    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= p + 3 ? min(p + 4, col_blocks - 1) : cc);
+    const unsigned col = (unsigned)(TLOD_NMS_TRI && c <= p + 2 ? min(p + 3, col_blocks - 1) : cc);
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if ((kg >> j) & 1u) r[j] = word((unsigned)(p * 64 + g * 16 + j), col);
   };
   load_w0(0, d0, n0);
-  load_w0(1, d1, n1);
   __syncthreads();
 
-  // Unrolled x3 below so the register sets never move (a copy of a register with a load
+  // Unrolled x2 below so the register sets never move (a copy of a register with a load
   // in flight would wait for that load): iteration b loads rows of block b-1 into set
-  // (b-1) % 3 and uses set b % 3 (block b-3's rows).
-  auto step = [&](int b, unsigned long long dcur, const unsigned long long (&ncur)[3],
-                  unsigned long long& dnext, unsigned long long (&nnext)[3],
+  // (b-1) % 2 and uses set b % 2 (block b-2's rows).
+  auto step = [&](int b, unsigned long long dcur, const unsigned long long (&ncur)[2],
+                  unsigned long long& dnext, unsigned long long (&nnext)[2],
                   unsigned long long (&rload)[16], const unsigned long long (&ruse)[16]) -> bool {
     if (b >= 1) load_rows(b - 1, s_kept[(b - 1) & 3], rload);
-    load_w0(b + 2, dnext, nnext);
+    load_w0(b + 1, dnext, nnext);
     if (t < 64) {  // wave 0: resolve block b
       const int valid = min(n - b * 64, 64);
       const unsigned long long vmask = valid == 64 ? ~0ull : ((1ull << valid) - 1ull);
@@ -168,7 +166,7 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
       if ((kept >> t) & 1ull) {
         keep[total + __popcll(kept & ((1ull << t) - 1ull))] = b * 64 + t;
 #pragma unroll
-        for (int q = 0; q < 3; ++q)  // near columns b+1..b+3
+        for (int q = 0; q < 2; ++q)  // near columns b+1, b+2
           if (b + 1 + q < col_blocks && ncur[q]) atomicOr(&remv[b + 1 + q], ncur[q]);
       }
       if (t == 0) {
@@ -177,8 +175,8 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
         if (max_keep > 0 && total + kc >= max_keep) s_done = 1;
       }
     }
-    if (b >= 3) {  // block b-3's survivors into the columns beyond b
-      const unsigned kg = (unsigned)(s_kept[(b - 3) & 3] >> (g * 16)) & 0xffffu;
+    if (b >= 2) {  // block b-2's survivors into the columns beyond b
+      const unsigned kg = (unsigned)(s_kept[(b - 2) & 3] >> (g * 16)) & 0xffffu;
       if (kg && c > b && c < col_blocks) {
         unsigned long long v = 0ull;
 #pragma unroll
@@ -189,10 +187,9 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
     __syncthreads();
     return s_done != 0;
   };
-  for (int b = 0; b < col_blocks; b += 3) {
-    if (step(b, d0, n0, d2, n2, r2, r0) || b + 1 >= col_blocks) break;
-    if (step(b + 1, d1, n1, d0, n0, r0, r1) || b + 2 >= col_blocks) break;
-    if (step(b + 2, d2, n2, d1, n1, r1, r2)) break;
+  for (int b = 0; b < col_blocks; b += 2) {
+    if (step(b, d0, n0, d1, n1, r1, r0) || b + 1 >= col_blocks) break;
+    if (step(b + 1, d1, n1, d0, n0, r0, r1)) break;
   }
   if (t == 0) *num_keep = s_total;
 }
