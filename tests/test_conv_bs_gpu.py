@@ -347,3 +347,38 @@ def test_conv3x3_direct(N, Cin, Cout, H, W):
         ref = F.relu(ref) if relu else ref
         got = y.double().cpu()
         assert float((got - ref).norm() / ref.norm()) < 1e-6
+
+
+def _ref_pack(w, dgrad):
+    """The packed split-bf16 planes of tlod_conv_pack_bs (conv.hip pack_bs_kernel) built with
+    torch ops: rows x chunks x 10 tap slots x 8 channels per plane, dgrad = the transposed,
+    tap-flipped operand; hi = the truncated bf16 of w, mid / lo the round-to-nearest-even
+    bf16 of the remainders (bs_common.h split2)."""
+    Cout, Cin = w.shape[:2]
+    a = w.permute(1, 0, 2, 3).flip(2, 3) if dgrad else w
+    rows, ins = a.shape[:2]
+    nch = (ins + 7) // 8
+    A = torch.zeros(rows, nch * 8, 10, dtype=torch.float32)
+    A[:, :ins, :9] = a.reshape(rows, ins, 9)
+    A = A.view(rows, nch, 8, 10).permute(0, 1, 3, 2).contiguous().view(-1)
+    u = A.view(torch.int32)
+    hi = (u & -65536).view(torch.float32)
+    r = A - hi
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return torch.cat([(u >> 16).to(torch.int16), mid.view(torch.int16), lo.view(torch.int16)])
+
+
+@pytest.mark.parametrize("Cout,Cin", [(64, 3), (64, 64), (128, 64), (512, 512), (20, 13),
+                                      (132, 130), (33, 517)])
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_pack_bs_bit_exact(Cout, Cin, dgrad):
+    """tlod_conv_pack_bs bit-exact vs the torch construction, including ragged channel
+    counts (Cin / Cout not a multiple of 8) and the dgrad transpose + tap flip."""
+    from tlod.conv import _pack_bs
+    g = torch.Generator().manual_seed(Cout * 1000 + Cin)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * torch.exp(torch.randn(Cout, Cin, 3, 3, generator=g))
+    p = _pack_bs(w.to(dev), dgrad).view(torch.int16).cpu()
+    ref = _ref_pack(w, dgrad)
+    assert p.numel() == ref.numel()
+    assert torch.equal(p, ref)
