@@ -766,10 +766,12 @@ constexpr int kProdWaves = 4;
 #if TLOD_WS_STAMPS
 __device__ unsigned long long g_ws_stamps[256 * 12 * 10];
 __device__ unsigned long long g_ws_clock[512];
+__device__ unsigned long long g_ws_tl[8192 * 2];  // per block: start, end (s_memrealtime)
 #define WS_STAMP_DECL                                \
   unsigned long long ws_seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
   const unsigned long long ws_t0 = __builtin_amdgcn_s_memtime(); \
   const unsigned long long ws_r0 = __builtin_amdgcn_s_memrealtime(); \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_ws_tl[blockIdx.x * 2] = ws_r0; \
   unsigned long long ws_t = ws_t0
 #define WS_STAMP(k)                                              \
   do {                                                           \
@@ -782,6 +784,8 @@ __device__ unsigned long long g_ws_clock[512];
     if (blockIdx.x < 256 && (threadIdx.x & 63) == 0)                             \
       for (int k_ = 0; k_ < 10; ++k_)                                            \
         g_ws_stamps[(blockIdx.x * 12 + threadIdx.x / 64) * 10 + k_] = ws_seg[k_]; \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                   \
+      g_ws_tl[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime();            \
     if (blockIdx.x < 256 && threadIdx.x == 0) {                                  \
       g_ws_clock[blockIdx.x * 2] = __builtin_amdgcn_s_memtime() - ws_t0;         \
       g_ws_clock[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime() - ws_r0; \
@@ -1022,21 +1026,26 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       if (c_begin + 1 < c_end) load2(S1, c_begin + 1);
       store2(S0, c_begin + 2);                          // chunk c_begin
       if (c_end - c_begin >= 2) store2(S1, c_begin + 3);  // chunk c_begin + 1
+      WS_STAMP(0);
       __syncthreads();
+      WS_STAMP(8);
       int c = c_begin;
+      // (stamp build: segment 0 = staging, k = wait at barrier Fk)
+#define WS_PSYNC(k) do { WS_STAMP(0); __syncthreads(); WS_STAMP(k); } while (0)
       for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {  // barriers as in the loop below
         if (c != c_begin) store2(S1, c + 3);  // chunk c+1
-        __syncthreads();
-        __syncthreads();
+        WS_PSYNC(1);
+        WS_PSYNC(2);
         store2(S0, c + 4);  // chunk c+2
-        __syncthreads();
-        __syncthreads();
+        WS_PSYNC(3);
+        WS_PSYNC(4);
         store2(S1, c + 5);  // chunk c+3
-        __syncthreads();
-        __syncthreads();
+        WS_PSYNC(5);
+        WS_PSYNC(6);
         if (c + 4 < c_end) store2(S0, c + 6);  // chunk c+4
-        __syncthreads();
+        WS_PSYNC(7);
       }
+#undef WS_PSYNC
       for (; c + 1 < c_end; c += 2) {
         if (c != c_begin) store2(S1, c + 3);  // chunk c+1
         __syncthreads();
@@ -1045,6 +1054,8 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
         __syncthreads();
       }
       if ((c_end - c_begin) & 1) __syncthreads();
+      WS_STAMP(0);
+      WS_STAMP_SAVE;
       return;
     }
     u32x4 ra[A_IT];
@@ -1278,7 +1289,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     for (int i = 0; i < RB; ++i)
 #pragma unroll
       for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    WS_STAMP(6);
+    WS_STAMP(0);
     __syncthreads();
     WS_STAMP(8);
     int c = it.c_begin;
@@ -1287,24 +1298,27 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     // units leave a 16x16x16 step, which issues at the 16x16x32's 16 cycles for half the
     // work (tools/probe/mfma_rate.hip), so whole frames run first.  Steps 2, 4 and 6 read
     // two chunks (both buffers); a buffer is refilled once its chunk's last step is done.
+    // (stamp build: segment 0 = k-steps, 1 = barrier waits)
+#define WS_SYNC(k) do { WS_STAMP(0); __syncthreads(); WS_STAMP(k); } while (0)
     for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {
       step16(aoff_s(0), boff_s(0));
       step16(aoff_s(1), boff_s(1));
-      __syncthreads();  // F1
+      WS_SYNC(1);  // F1
       step16(aoff_s(2), boff_s(2));
-      __syncthreads();  // F2
+      WS_SYNC(2);  // F2
       step16(aoff_s(3), boff_s(3));
-      __syncthreads();  // F3
+      WS_SYNC(3);  // F3
       step16(aoff_s(4), boff_s(4));
-      __syncthreads();  // F4
+      WS_SYNC(4);  // F4
       step16(aoff_s(5), boff_s(5));
-      __syncthreads();  // F5
+      WS_SYNC(5);  // F5
       step16(aoff_s(6), boff_s(6));
-      __syncthreads();  // F6
+      WS_SYNC(6);  // F6
       step16(aoff_s(7), boff_s(7));
       step16(aoff_s(8), boff_s(8));
-      __syncthreads();  // F7
+      WS_SYNC(7);  // F7
     }
+#undef WS_SYNC
     for (; c + 1 < c_end; c += 2) {
       WS_STAMP(-1);
       step16(aoff_s(0), boff_s(0));
@@ -1328,7 +1342,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       step8(aoffL, boffL);
       __syncthreads();
     }
-    WS_STAMP(9);
+    WS_STAMP(0);
 
     // epilogue: the lane holds rows 4g..4g+3 of column l16 of each 16 x 16 tile
     if (!it.direct) {
@@ -1445,7 +1459,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
             }
       }
     }
-    WS_STAMP(7);
+    WS_STAMP(9);
   }
   WS_STAMP_SAVE;
 }
@@ -2591,6 +2605,9 @@ extern "C" int tlod_debug_ws_stamps(unsigned long long* host) {
              ? 0
              : 1;
 }
+extern "C" int tlod_debug_ws_timeline(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_tl), sizeof(g_ws_tl)) == hipSuccess ? 0 : 1;
+}
 #endif
 
 extern "C" int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
@@ -2697,8 +2714,24 @@ static size_t wgrad_bs_ws(int sp, int Cin, int Cout, int KS) {
          (size_t)sp * Cout * sizeof(float);
 }
 
+namespace tlod {
+// csrc/wgrad_ws.hip: the warp-specialized 3x3 weight gradient (2D pixel-tile chunks)
+bool wgrad_ws_applies(int N, int Cin, int H, int W, int Cout, int KS, int nprod);
+size_t wgrad_ws_workspace(int N, int Cin, int H, int W, int Cout);
+int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int accumulate, int N,
+                    int Cin, int H, int W, int Cout, void* ws, size_t ws_bytes, hipStream_t s);
+int launch_db_reduce(const float* db_slab, int splits, int C, float* db, int accumulate,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(db_reduce_kernel, dim3(div_up(C, 256)), dim3(256), 0, s, db_slab, splits, C,
+                     db, accumulate);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+}  // namespace tlod
+
 extern "C" size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
                                                      int nprod) {
+  if (wgrad_ws_applies(N, Cin, H, W, Cout, KS, nprod)) return wgrad_ws_workspace(N, Cin, H, W, Cout);
   const int sp = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
   return sp > 0 ? wgrad_bs_ws(sp, Cin, Cout, KS) : 0;
 }
@@ -2715,6 +2748,8 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
   TLOD_CHECK_ARG((size_t)N * std::max(Cin, Cout) * H * W * 4 < (1ull << 31), "tensor too large");
   TLOD_CHECK_ARG((size_t)H * W < (1u << 21), "map too large");
   hipStream_t s = (hipStream_t)stream;
+  if (wgrad_ws_applies(N, Cin, H, W, Cout, KS, nprod))
+    return wgrad_ws_launch(dy, x, dw, db, accumulate, N, Cin, H, W, Cout, ws, ws_bytes, s);
   const int splits =
       with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
   if (ws_bytes < wgrad_bs_ws(splits, Cin, Cout, KS)) {
