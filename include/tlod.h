@@ -13,6 +13,19 @@
  *     launchers do: roi_align_kernel.cu:84-88);
  *   - tensors are contiguous NCHW float32 (the reference's layout and dtype).
  *
+ * Environment switches (read ONCE per process, at the first call that consults them; they
+ * choose between kernels that compute the same result — none is needed for correctness):
+ *   TLOD_ROI_BWD_GATHER=0  RoIAlignAvg backward on the atomic kernels instead of the
+ *                          deterministic sorted-tap gather (the gather workspace query then
+ *                          returns 0);
+ *   TLOD_ROI_BWD_LDS=1     with the gather off: the LDS-accumulation backward kernel;
+ *   TLOD_WGRAD_WS=0        3x3 bf16x6 weight gradient on the im2col kernel instead of the
+ *                          warp-specialized pixel-tile kernel;
+ *   TLOD_CONV_WS=0, TLOD_WS_MINCIN=n, TLOD_WS_FLEX=0, TLOD_WS_PERSIST=1, TLOD_CONV_BAND=0,
+ *   TLOD_CONV_FWD_CK=4, TLOD_CONV_WGRAD_TH=2
+ *                          split-bf16 / f32 conv forward tilings (see csrc/conv.hip);
+ * the workspace queries follow the same switches, so query after setting them.
+ *
  * Each entry point names the reference interface it replaces (paths relative to the
  * reference checkout).
  */
@@ -240,7 +253,8 @@ int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float* scale, fl
 
 /* ------------------------------------------------------------------ Split-bf16 3x3 conv
  * The forward / dgrad of tlod_conv_fwd_f32 on the bf16 MFMA: each f32 operand is split
- * exactly into three bf16 terms (x = hi + mid + lo, round-to-nearest) and nprod = 6 products
+ * exactly into three bf16 terms (x = hi + mid + lo: hi the truncated top 8 significant bits,
+ * mid and lo the round-to-nearest-even bf16 of the remainders) and nprod = 6 products
  * (hi*hi, hi*mid, mid*hi, hi*lo, mid*mid, lo*hi) are accumulated in f32 — error at the
  * level of f32 rounding (normwise ~1e-7 vs fp64, like the f32-input MFMA path) at up to
  * 2.7x its MFMA rate; nprod = 3 (hi*hi, hi*mid, mid*hi) trades that for ~5e-6.
@@ -258,11 +272,12 @@ int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float* scale, con
                          const float* residual, float* y, int N, int Cin, int H, int W, int Cout,
                          int KS, int relu, int nprod, void* ws, size_t ws_bytes,
                          tlod_stream_t stream);
-/* Split-bf16 wgrad: tlod_conv_wgrad_f32's result (same argument meaning, same
- * deterministic split-K slab reduction) with dy and x split into bf16 planes on the fly and
- * nprod (6 or 3) products on the bf16 MFMA.  No weight pack.  KS = 1 or 3.  db (optional,
- * Cout floats): the bias gradient sum_{n,h,w} dy, from the staged dy rows in the same
- * launch (replaces the bias-gradient half of the ReLU backward pass). */
+/* Split-bf16 wgrad: tlod_conv_wgrad_f32's result (same argument meaning, deterministic
+ * split-K slab reduction in fixed split order) with dy and x split into bf16 planes on the
+ * fly and nprod (6 or 3) products on the bf16 MFMA.  No weight pack.  KS = 1 or 3 (3x3 with
+ * nprod = 6: the warp-specialized kernel over 4 x 16 pixel tiles, csrc/wgrad_ws.hip).  db
+ * (optional, Cout floats): the bias gradient sum_{n,h,w} dy, from the staged dy rows in the
+ * same launch (replaces the bias-gradient half of the ReLU backward pass). */
 size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
                                           int nprod);
 int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, float* db, int accumulate,

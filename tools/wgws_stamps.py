@@ -24,7 +24,7 @@ f.argtypes = [ctypes.c_void_p]
 assert f(buf.ctypes.data) == 0
 a = buf[:256 * 48].reshape(256, 12, 4).astype(np.float64)
 for role, sl, names in (("MFMA waves", slice(0, 8), ["k-steps", "barrier waits", "epilogue", "first barrier"]),
-                        ("producer waves", slice(8, 12), ["staging", "barrier waits", "-", "-"])):
+                        ("producer waves", slice(8, 12), ["staging", "barrier waits", "load wait", "-"])):
     v = a[:, sl, :]
     tot = v.sum(-1)
     print(f"{role}: total cycles per wave median {np.median(tot):.0f}")

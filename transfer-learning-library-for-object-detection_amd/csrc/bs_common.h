@@ -42,15 +42,26 @@ __device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
 __device__ __forceinline__ float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
 
+// f32 subtraction the compiler cannot SLP-pack into v_pk_add_f32: on gfx950 the packed f32
+// ops are an anti-lever beside MFMAs (MI355X_MICROARCH.md, constants table: +22-26 cycles
+// per packed op in an MFMA stream), and a producer wave sharing its SIMD with MFMA waves
+// issued them at a fraction of the plain rate (wgrad_ws producers: ~48 cycles per
+// instruction with the compiler's packed split).
+__device__ __forceinline__ float sub_f32(float a, float b) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // one pair of floats -> its NPL packed bf16 planes
 template <int NPL>
 __device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m,
                                        unsigned& l) {
   const unsigned u0 = __float_as_uint(x0) & 0xffff0000u, u1 = __float_as_uint(x1) & 0xffff0000u;
   h = (u0 >> 16) | u1;  // v_perm_b32
-  const float r0 = x0 - __uint_as_float(u0), r1 = x1 - __uint_as_float(u1);
+  const float r0 = sub_f32(x0, __uint_as_float(u0)), r1 = sub_f32(x1, __uint_as_float(u1));
   m = cvt_pk_bf16(r0, r1);
-  if constexpr (NPL == 3) l = cvt_pk_bf16(r0 - bf_lo(m), r1 - bf_hi(m));
+  if constexpr (NPL == 3) l = cvt_pk_bf16(sub_f32(r0, bf_lo(m)), sub_f32(r1, bf_hi(m)));
 }
 
 // split 8 floats into NPL bf16 planes (16 B each)

@@ -1465,7 +1465,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 }
 
 // Packed, pre-split weights for conv_fwd_bs_kernel: three bf16 planes (hi, mid, lo of the
-// exact round-to-nearest split), each P[pl][o][c*80 + s*8 + e] = weight of output row o, input
+// exact split: truncated hi, round-to-nearest-even mid and lo; bs_common.h split2), each P[pl][o][c*80 + s*8 + e] = weight of output row o, input
 // channel c*8+e, tap s (0 for s = 9 — the pad tap — and past the last channel).  dgrad = 1
 // packs the transposed, flipped operand (rows = input channels, inputs = output channels,
 // tap 8-s).

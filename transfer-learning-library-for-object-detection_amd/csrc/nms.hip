@@ -88,13 +88,15 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
     int32_t* __restrict__ num_keep) {
   __shared__ unsigned long long remv[kFastColBlocks];
   __shared__ unsigned long long s_kept[4];
-  __shared__ int s_total, s_done;
+  // s_done is double-buffered by block parity: thread 0 may set block b+1's flag before a
+  // slower wave has read block b's after the barrier (a single flag would be a data race)
+  __shared__ int s_total, s_done[2];
   const int t = threadIdx.x;
   const int c = t & 255, g = t >> 8;
   const int cc = min(c, col_blocks - 1);  // clamped column (masked later)
   if (t < kFastColBlocks) remv[t] = 0ull;
   if (t < 4) s_kept[t] = 0ull;
-  if (t == 0) { s_total = 0; s_done = 0; }
+  if (t == 0) { s_total = 0; s_done[0] = s_done[1] = 0; }
 
   // Iteration b: wave 0 resolves block b, then ORs its survivors' words of columns b+1, b+2
   // into remv itself (from 2 words per lane it prefetched: the near columns); meanwhile
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
       if (t == 0) {
         s_kept[b & 3] = kept;
         s_total = total + kc;
-        if (max_keep > 0 && total + kc >= max_keep) s_done = 1;
+        if (max_keep > 0 && total + kc >= max_keep) s_done[b & 1] = 1;
       }
     }
     if (b >= 2) {  // block b-2's survivors into the columns beyond b
@@ -185,7 +187,7 @@ __global__ void __launch_bounds__(kScanThreads) nms_scan_fast_kernel(
       }
     }
     __syncthreads();
-    return s_done != 0;
+    return s_done[b & 1] != 0;
   };
   for (int b = 0; b < col_blocks; b += 2) {
     if (step(b, d0, n0, d1, n1, r1, r0) || b + 1 >= col_blocks) break;

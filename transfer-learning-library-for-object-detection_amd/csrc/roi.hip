@@ -667,8 +667,19 @@ extern "C" size_t tlod_roi_align_avg_bwd_workspace_bytes(int B, int C, int H, in
   return (size_t)B * C * H * W * sizeof(float);
 }
 
+// The sorted-tap gather backward is the default; TLOD_ROI_BWD_GATHER=0 (read once per process,
+// documented in tlod.h) selects the atomic kernels, and then the gather needs no workspace.
+static bool roi_bwd_gather_on() {
+  static const bool on = [] {
+    const char* v = getenv("TLOD_ROI_BWD_GATHER");
+    return !(v && *v == '0');
+  }();
+  return on;
+}
+
 extern "C" size_t tlod_roi_align_avg_bwd_gather_workspace_bytes(int B, int C, int H, int W, int R,
                                                                int ph, int pw) {
+  if (!roi_bwd_gather_on()) return 0;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || R <= 0 || ph <= 0 || pw <= 0) return 0;
   Carve cv(nullptr, 0);
   RbgWs w;
@@ -683,10 +694,8 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
   TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
   if (R == 0) return kOk;
   hipStream_t s = (hipStream_t)stream;
-  // the sorted-tap gather by default (177 vs 243 us on the DAF step's RoIs, deterministic);
-  // TLOD_ROI_BWD_GATHER=0: the atomic kernels (read per call)
-  const char* gv = getenv("TLOD_ROI_BWD_GATHER");
-  const bool gather_off = gv && *gv == '0';
+  // the sorted-tap gather by default (deterministic); TLOD_ROI_BWD_GATHER=0: the atomic kernels
+  const bool gather_off = !roi_bwd_gather_on();
   const size_t ncell_sz = (size_t)B * H * W;
   if (!gather_off && ws != nullptr && ncell_sz < (1u << 31) &&
       ws_bytes >= tlod_roi_align_avg_bwd_gather_workspace_bytes(B, C, H, W, R, ph, pw)) {

@@ -34,7 +34,11 @@ namespace tlod {
 namespace wgws {
 constexpr int BM = 128, BC = 32, TH = 4, TW = 16, KC = TH * TW;  // K chunk = 64 pixels
 constexpr int PH = TH + 2, PW = TW + 2, PP = PH * PW;              // 6 x 18 = 108 positions
-constexpr int NMW = 8, NPW = 4;                                    // MFMA / producer waves
+#ifndef TLOD_WGWS_NPW  // producer waves per workgroup (4: 3 waves per SIMD; 8: 4 per SIMD)
+#define TLOD_WGWS_NPW 4
+#endif
+constexpr int NMW = 8, NPW = TLOD_WGWS_NPW;                        // MFMA / producer waves
+constexpr int WAVES_PER_SIMD = (NMW + NPW) / 4;
 constexpr int NT = (NMW + NPW) * 64;
 constexpr int A_ROW = KC * 2;                 // 128 B per co row per plane
 constexpr int A_PLANE = BM * A_ROW;           // 16384
@@ -45,7 +49,7 @@ constexpr int BUF = A_BYTES + B_BYTES;        // 72192
 constexpr int LDS_BYTES = 2 * BUF;            // 144384
 constexpr int TILE_FLOATS = BM * BC * 9;      // partial tile per workgroup (36864)
 constexpr int A_ITEMS = BM * TH * 2;          // (co, tile row, 8-pixel half)
-constexpr int A_IT = A_ITEMS / (NPW * 64);    // 4
+constexpr int A_IT = A_ITEMS / (NPW * 64);    // 4 (NPW = 4)
 constexpr int B_ITEMS = (BC / 8) * PP;        // (octet, position) = 432
 constexpr int B_IT = (B_ITEMS + NPW * 64 - 1) / (NPW * 64);  // 2
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -59,6 +63,9 @@ static_assert(A_ITEMS % (NPW * 64) == 0, "A staging");
 // split (raw bits stored), 3 = no LDS stores.
 #ifndef TLOD_WGWS_ABL
 #define TLOD_WGWS_ABL 0
+#endif
+#ifndef TLOD_WGWS_BSPLIT  // 1: the MFMA waves stage B (the X patch), the producers only A
+#define TLOD_WGWS_BSPLIT 1
 #endif
 #ifndef TLOD_WGWS_PRIO  // s_setprio of the producer waves (0: default)
 #define TLOD_WGWS_PRIO 0
@@ -127,6 +134,7 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
                                              int per_img, int ptid) {
   using namespace wgws;
   if (TLOD_WGWS_PRIO) __builtin_amdgcn_s_setprio(TLOD_WGWS_PRIO);
+  WG_STAMP_DECL;
   const int HW = H * W;
   const i32x4 g_rsrc = make_buffer_rsrc(G, (unsigned)((size_t)N * Cout * HW * 4));
   const i32x4 x_rsrc = make_buffer_rsrc(X, (unsigned)((size_t)N * Cin * HW * 4));
@@ -134,7 +142,7 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
   int a_lds[A_IT], a_co[A_IT];
 #pragma unroll
   for (int i = 0; i < A_IT; ++i) {
-    const int co_l = (ptid >> 3) + 32 * i;
+    const int co_l = (ptid >> 3) + NPW * 8 * i;
     a_lds[i] = co_l * A_ROW + 16 * (a_s ^ (co_l & 7));
     a_co[i] = m0 + co_l < Cout ? m0 + co_l : -1;
   }
@@ -156,7 +164,9 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
   f32x4v ra[2][A_IT][2];
   float rb[2][B_IT][8];
   int anv[2];  // valid pixels of this lane's two 4-pixel A quads (edge chunks), else 4
-  // load cursor: image ln, tile origin (lh0, lw0) of the next chunk to load
+  // load cursor: image ln, tile origin (lh0, lw0) of the next chunk to load; ld_left chunks
+  // of the range remain (loads past it read out of range: zeros, never consumed)
+  int ld_left = nch;
   int ln = c_begin / per_img;
   int lh0, lw0;
   {
@@ -168,20 +178,21 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
     constexpr int S = decltype(slc)::value;
     anv[S] = min(max(W - (lw0 + a_px), 0), 4);
     const int w = lw0 + a_px;
+    const bool live = ld_left-- > 0;
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int h = lh0 + a_rr + 2 * hh;
-        const int off = a_co[i] >= 0 && h < H && w < W ? (((ln * Cout + a_co[i]) * H + h) * W + w) * 4 : kBufOOB;
+        const int off = live && a_co[i] >= 0 && h < H && w < W ? (((ln * Cout + a_co[i]) * H + h) * W + w) * 4 : kBufOOB;
         ra[S][i][hh] = TLOD_WGWS_ABL == 1 ? f32x4v{(float)off, 1.f, 2.f, 3.f}
                                           : raw_buffer_load_v4f32(g_rsrc, off, 0, 0);
       }
     }
 #pragma unroll
-    for (int i = 0; i < B_IT; ++i) {
+    for (int i = 0; i < (TLOD_WGWS_BSPLIT ? 0 : B_IT); ++i) {
       const int gh = lh0 + b_pr[i], gw = lw0 + b_pc[i];
-      const bool ok = b_lds[i] >= 0 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+      const bool ok = live && b_lds[i] >= 0 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
       const int off = ok ? ((ln * Cin + b_ci[i]) * HW + gh * W + gw) * 4 : kBufOOB;
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -216,6 +227,11 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
   };
   auto store = [&](auto slc, unsigned char* buf) {
     constexpr int S = decltype(slc)::value;
+#if TLOD_WGWS_STAMPS  // diagnostic: the wait for this slot's loads as a segment of its own
+    WG_STAMP(0);
+    if (TLOD_WGWS_BSPLIT) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    WG_STAMP(2);
+#endif
     const int nv = anv[S];
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
@@ -235,7 +251,7 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
       put(buf + a_lds[i], A_PLANE, v);
     }
 #pragma unroll
-    for (int i = 0; i < B_IT; ++i) {
+    for (int i = 0; i < (TLOD_WGWS_BSPLIT ? 0 : B_IT); ++i) {
       if (b_lds[i] < 0) continue;
       float v[8];
 #pragma unroll
@@ -249,31 +265,27 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
   };
   const std::integral_constant<int, 0> S0;
   const std::integral_constant<int, 1> S1;
-  WG_STAMP_DECL;
-  if (nch > 0) load(S0);
-  if (nch > 1) load(S1);
-  if (nch > 0) {
-    store(S0, smem);
-    if (nch > 2) load(S0);
-  }
+  // Straight-line pairs of iterations (loads and stores unconditional: a store past the range
+  // goes to the buffer nobody reads next, a load past it reads zeros), so the compiler's
+  // vmcnt waits before a store leave the other slot's 8 loads in flight.  2 * ceil(nch / 2)
+  // + 1 barriers, as the MFMA waves.
+  load(S0);
+  load(S1);
+  store(S0, smem);
+  load(S0);
   WG_STAMP(0);
   __syncthreads();
   WG_STAMP(1);
   for (int j = 0; j < nch; j += 2) {
     // iteration j: the MFMA waves read chunk j (buffer 0); stage chunk j + 1 (buffer 1)
-    if (j + 1 < nch) {
-      store(S1, smem + BUF);
-      if (j + 3 < nch) load(S1);
-    }
+    store(S1, smem + BUF);
+    load(S1);
     WG_STAMP(0);
     __syncthreads();
     WG_STAMP(1);
-    if (j + 1 >= nch) break;
     // iteration j + 1: stage chunk j + 2 (buffer 0)
-    if (j + 2 < nch) {
-      store(S0, smem);
-      if (j + 4 < nch) load(S0);
-    }
+    store(S0, smem);
+    load(S0);
     WG_STAMP(0);
     __syncthreads();
     WG_STAMP(1);
@@ -293,7 +305,8 @@ __device__ __forceinline__ void wgws_produce(const float* __restrict__ G, const 
 // Grid: tiles_m x tiles_c x splits workgroups; workgroup (mt, ct, split) owns output
 // channels [128 mt, +128), input channels [32 ct, +32) and pixel-tile chunks
 // [split * cps, +cps) of the N x ceil(H/4) x ceil(W/16) chunk grid.
-__global__ void __launch_bounds__(wgws::NT) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ void __launch_bounds__(wgws::NT)
+    __attribute__((amdgpu_waves_per_eu(wgws::WAVES_PER_SIMD, wgws::WAVES_PER_SIMD)))
 wgrad_ws_kernel(const float* __restrict__ G, const float* __restrict__ X,
                 float* __restrict__ slab, float* __restrict__ db_slab, int N, int Cin, int H,
                 int W, int Cout, int tiles_m, int tiles_c, int splits, int cps) {
@@ -369,16 +382,86 @@ wgrad_ws_kernel(const float* __restrict__ G, const float* __restrict__ X,
       }
     }
   };
+  // B staging by the MFMA waves (TLOD_WGWS_BSPLIT): lane tid < 432 owns one (octet,
+  // position) item of the patch; chunk j's 8 channel values are loaded two chunks ahead
+  // into register slot j & 1 and split + stored between the two k-steps of chunk j - 1
+  const bool b_item = TLOD_WGWS_BSPLIT && tid < B_ITEMS;
+  const int b_oct = tid / PP, b_pos = tid % PP;
+  const int b_lds = b_oct * B_OCT + b_pos * 16;
+  const int b_pr = b_pos / PW - 1, b_pc = b_pos % PW - 1, b_ci = c0 + 8 * b_oct;
+  const int HW = H * W;
+  const i32x4 x_rsrc = make_buffer_rsrc(X, (unsigned)((size_t)N * Cin * HW * 4));
+  const bool cmask = (Cin & 7) != 0;
+  float rbv[2][8];
+  int ld_left = nch;
+  int ln = c_begin / per_img, lh0, lw0;
+  {
+    const int r = c_begin - ln * per_img;
+    lh0 = (r / tcols) * TH;
+    lw0 = (r % tcols) * TW;
+  }
+  auto loadB = [&](auto slc) {
+    constexpr int S = decltype(slc)::value;
+    const int gh = lh0 + b_pr, gw = lw0 + b_pc;
+    const bool ok = ld_left-- > 0 && b_item && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+    const int off = ok ? ((ln * Cin + b_ci) * HW + gh * W + gw) * 4 : kBufOOB;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rbv[S][e] = raw_buffer_load_f32(x_rsrc, off, e * HW * 4, 0);
+    lw0 += TW;
+    if (lw0 >= W) {
+      lw0 = 0;
+      lh0 += TH;
+      if (lh0 >= H) {
+        lh0 = 0;
+        ++ln;
+      }
+    }
+  };
+  auto storeB = [&](auto slc, unsigned char* buf) {
+    constexpr int S = decltype(slc)::value;
+    if (!b_item) return;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = rbv[S][e];
+    if (cmask) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = b_ci + e < Cin ? v[e] : 0.f;
+    }
+    u32x4 sp[3];
+    split8<3>(v, sp);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      *reinterpret_cast<u32x4*>(buf + A_BYTES + pl * B_PLANE + b_lds) = sp[pl];
+  };
+  const std::integral_constant<int, 0> S0;
+  const std::integral_constant<int, 1> S1;
   WG_STAMP_DECL;
+  if (TLOD_WGWS_BSPLIT) {  // unconditional, as the producers' (see wgws_produce)
+    loadB(S0);
+    loadB(S1);
+    storeB(S0, smem);
+    loadB(S0);
+  }
   __syncthreads();
   WG_STAMP(3);
-  for (int j = 0; j < nch; ++j) {
-    const unsigned char* buf = smem + (j & 1) * BUF;
-    kstep(buf, a_s0, b_lane);
-    kstep(buf, a_s1, b_lane + PW * 16);  // k rows 32..63: tile rows 1 and 3
+  // iteration j reads buffer j & 1 and stages chunk j + 1's B into buffer (j + 1) & 1; the
+  // odd count's last iteration computes nothing (its barrier pairs the producers')
+  auto iter = [&](auto slc_next, int j) {
+    unsigned char* buf = smem + (j & 1) * BUF;
+    const bool live = j < nch;
+    if (live) kstep(buf, a_s0, b_lane);
+    if (TLOD_WGWS_BSPLIT) {
+      storeB(slc_next, smem + ((j + 1) & 1) * BUF);
+      loadB(slc_next);
+    }
+    if (live) kstep(buf, a_s1, b_lane + PW * 16);  // k rows 32..63: tile rows 1 and 3
     WG_STAMP(0);
     __syncthreads();
     WG_STAMP(1);
+  };
+  for (int j = 0; j < nch; j += 2) {
+    iter(S1, j);
+    iter(S0, j + 1);
   }
   // partial tile in lane order: [wave][i][t][lane][4]
   float* S = slab + ((size_t)split * tiles + tile) * TILE_FLOATS + (size_t)w * (2 * 9 * 256) + lane * 4;

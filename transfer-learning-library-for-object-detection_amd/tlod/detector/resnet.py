@@ -30,19 +30,22 @@ from ..linear import LinearFunction, linear_math
 
 def fold_bn(bn):
     """Frozen eval-mode BatchNorm as y = x * scale + shift (per channel).  Cached on the
-    module and recomputed only when one of its four tensors changes (pointer or in-place
-    version): ResNet101 has 104 BatchNorms, i.e. 400+ small launches per forward otherwise."""
+    module and recomputed only when one of its four tensors changes: a different tensor object
+    (reassignment, load_state_dict(assign=True)) or an in-place write (its version counter).
+    The cache holds the four tensors themselves, so a replaced tensor's storage cannot be
+    reused at the same address while its fold is cached.  ResNet101 has 104 BatchNorms, i.e.
+    400+ small launches per forward otherwise."""
     assert not bn.weight.requires_grad, "tlod ResNet expects frozen BatchNorm (resnet.py:261-267)"
     ts = (bn.weight, bn.bias, bn.running_mean, bn.running_var)
-    k = tuple((t.data_ptr(), t._version) for t in ts) + (bn.eps,)
+    vs = tuple(t._version for t in ts) + (bn.eps,)
     c = getattr(bn, "_tlod_fold", None)
-    if c is not None and c[0] == k:
-        return c[1], c[2]
+    if c is not None and c[1] == vs and all(a is b for a, b in zip(c[0], ts)):
+        return c[2], c[3]
     with torch.no_grad():
         scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
         shift = bn.bias - bn.running_mean * scale
     scale, shift = scale.contiguous(), shift.contiguous()
-    bn._tlod_fold = (k, scale, shift)
+    bn._tlod_fold = (ts, vs, scale, shift)
     return scale, shift
 
 
