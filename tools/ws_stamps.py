@@ -24,8 +24,8 @@ f = _lib.lib().tlod_debug_ws_stamps
 f.argtypes = [ctypes.c_void_p]
 assert f(buf.ctypes.data) == 0
 a = buf[:256 * 12 * 10].reshape(256, 12, 10).astype(np.float64)
-names = ["work (k-steps | staging)", "wait F1", "wait F2", "wait F3", "wait F4", "wait F5",
-         "wait F6", "wait F7", "first barrier", "epilogue"]
+names = ["work (k-steps | staging)", "wait F1 (flags: all waits)", "wait F2", "wait F3", "wait F4",
+         "wait F5", "wait F6", "wait F7", "first barrier", "epilogue"]
 for role, sl in (("MFMA waves", slice(0, 8)), ("producer waves", slice(8, 12))):
     v = a[:, sl, :]
     tot = v.sum(-1)

@@ -763,6 +763,31 @@ constexpr int kProdWaves = 4;
 #ifndef TLOD_WS_DEPTH2  // producers two chunks ahead in registers (one-item mode)
 #define TLOD_WS_DEPTH2 1
 #endif
+// TLOD_WS_FLAGS=1 (one-item mode): producers and MFMA waves hand the two LDS buffers over
+// through counters in LDS instead of workgroup barriers — the producers store chunk j into
+// buffer j & 1 once every MFMA wave has retired chunk j - 2 from it and count it ready; an
+// MFMA wave waits only for the chunk its next k-step reads.  Measured slower (round 4,
+// conv3_3 shape, one lease: fwd 0.50 vs 0.47 ms, dgrad 0.447 vs 0.408): the MFMA waves drift
+// apart, the slowest one gates the producers' refill of a buffer, and with two buffers the
+// refill window shrinks (MFMA waves 26% and producers 67% of their cycles in the waits).
+#ifndef TLOD_WS_FLAGS
+#define TLOD_WS_FLAGS 0
+#endif
+// counter wait with a bounded spin: a miscounted protocol ends the kernel (wrong results,
+// caught by the tests) instead of hanging the GPU
+__device__ __forceinline__ void ws_wait_ge(const int* ctr, int target) {
+  for (int it = 0; it < (1 << 22); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");  // the reads that follow stay behind the poll
+}
+// one add per wave, after all of the wave's LDS operations so far have completed (LDS is
+// one coherent memory: a wave that sees the count sees the data / the retired reads)
+__device__ __forceinline__ void ws_signal(int* ctr) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 #if TLOD_WS_STAMPS
 __device__ unsigned long long g_ws_stamps[256 * 12 * 10];
 __device__ unsigned long long g_ws_clock[512];
@@ -817,7 +842,8 @@ struct WsCfg : BsCfg<WM, WN, MI, NJ, NP, false> {
   static constexpr int B_PLANE = BPOS * 16;
   static constexpr int BUF0 = B::NPL * (A_PLANE + B_PLANE);
   static constexpr int BUF = (BUF0 / 16) % 2 == 0 ? BUF0 + 16 : BUF0;
-  static constexpr int LDS_BYTES = 2 * BUF + 4 * B::BM * 4;
+  static constexpr int CTR = 2 * BUF + 4 * B::BM * 4;  // ready[2], retired[2] (TLOD_WS_FLAGS)
+  static constexpr int LDS_BYTES = CTR + 16;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -976,49 +1002,49 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       // p + 2 into the slot — a chunk's loads have two chunk-steps to land instead of one.
       set_ld_item();
       const int c_begin = ld.c_begin, c_end = ld.c_end;
-      unsigned am = 0, bm = 0;
+      // raw buffer loads, no element masks: rows past Cout and positions outside the map
+      // take offset kBufOOB, channels past Cin fall past the image's range — all read 0
+      // (fewer producer VALU than 64-bit flat addresses + selects: no 64-bit address math)
+      int a_vo[A_IT], b_vo[B_IT];
 #pragma unroll
-      for (int i = 0; i < A_IT; ++i) am |= (unsigned)(a_off[i] >= 0) << i;
+      for (int i = 0; i < A_IT; ++i) a_vo[i] = a_off[i] >= 0 ? a_off[i] : kBufOOB;
 #pragma unroll
-      for (int i = 0; i < B_IT; ++i) bm |= (unsigned)(b_goff[i] >= 0) << i;
-      const float* Xn = X + (size_t)ld.n * Cin * HWi;
+      for (int i = 0; i < B_IT; ++i) b_vo[i] = b_goff[i] >= 0 ? b_goff[i] * 4 : kBufOOB;
       u32x4 ra2[2][A_IT];
       float rb2[2][B_IT][8];
-      int nv2[2] = {8, 8};
-      auto load2 = [&](auto slc, int ch) {  // chunk ch -> slot S (unconditional, masked at store)
+      auto load2 = [&](auto slc, int ch) {  // chunk ch -> slot S (unconditional)
         constexpr int S = decltype(slc)::value;
-        const int ci0 = ch * C::CK;
-        const int nv = min(C::CK, Cin - ci0);
-        const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp) + ch * (kBsKP * 2);
+        const int cbytes = ch * C::CK * HWi * 4;
 #pragma unroll
-        for (int i = 0; i < A_IT; ++i) ra2[S][i] = *reinterpret_cast<const u32x4*>(Wb + max(a_off[i], 0));
-        const float* Xc = Xn + (size_t)ci0 * HWi;
+        for (int i = 0; i < A_IT; ++i)
+          ra2[S][i] = __builtin_bit_cast(u32x4, raw_buffer_load_v4f32(w_rsrc, a_vo[i], ch * (kBsKP * 2), 0));
 #pragma unroll
         for (int i = 0; i < B_IT; ++i)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) rb2[S][i][e] = Xc[min(e, nv - 1) * HWi + max(b_goff[i], 0)];
-        nv2[S] = nv;
+          for (int e = 0; e < 8; ++e)
+            rb2[S][i][e] = raw_buffer_load_f32(x_rsrc, b_vo[i], cbytes + e * HWi * 4, 0);
       };
       auto store2 = [&](auto slc, int ch_next) {  // slot S -> LDS buffer S; load ch_next into S
         constexpr int S = decltype(slc)::value;
         unsigned char* buf = smem + S * C::BUF;
 #pragma unroll
         for (int i = 0; i < A_IT; ++i)
-          if (a_lds[i] >= 0)
-            *reinterpret_cast<u32x4*>(buf + a_lds[i]) = ((am >> i) & 1) ? ra2[S][i] : u32x4{0, 0, 0, 0};
+          if (a_lds[i] >= 0) *reinterpret_cast<u32x4*>(buf + a_lds[i]) = ra2[S][i];
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
           if (b_pos[i] < 0) continue;
           u32x4 sp[3];
           float v8[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v8[e] = (((bm >> i) & 1) && e < nv2[S]) ? rb2[S][i][e] : 0.f;
+          for (int e = 0; e < 8; ++e) v8[e] = rb2[S][i][e];
           split8<C::NPL>(v8, sp);
 #pragma unroll
           for (int pl = 0; pl < C::NPL; ++pl)
             *reinterpret_cast<u32x4*>(buf + b_pos[i] + pl * C::B_PLANE) = sp[pl];
         }
-        if (ch_next < c_end) load2(slc, ch_next);
+        // unconditional (a chunk past the item reads zeros / stale pack rows, never stored),
+        // so the compiler's vmcnt waits keep the other slot's loads in flight
+        load2(slc, ch_next);
       };
       const std::integral_constant<int, 0> S0;
       const std::integral_constant<int, 1> S1;
@@ -1029,6 +1055,27 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       WS_STAMP(0);
       __syncthreads();
       WS_STAMP(8);
+      if (TLOD_WS_FLAGS) {
+        // chunks 0 and 1 are covered by the barrier (the counters start at one use each)
+        int* ready = reinterpret_cast<int*>(smem + C::CTR);
+        int* retired = ready + 2;
+        const int n = c_end - c_begin;
+        for (int j = 2; j < n; j += 2) {
+          ws_wait_ge(&retired[0], 8 * (j >> 1));  // chunk j - 2 retired from buffer 0
+          WS_STAMP(1);
+          store2(S0, c_begin + j + 2);
+          ws_signal(&ready[0]);
+          WS_STAMP(0);
+          if (j + 1 >= n) break;
+          ws_wait_ge(&retired[1], 8 * (j >> 1));
+          WS_STAMP(1);
+          store2(S1, c_begin + j + 3);
+          ws_signal(&ready[1]);
+          WS_STAMP(0);
+        }
+        WS_STAMP_SAVE;
+        return;
+      }
       int c = c_begin;
       // (stamp build: segment 0 = staging, k = wait at barrier Fk)
 #define WS_PSYNC(k) do { WS_STAMP(0); __syncthreads(); WS_STAMP(k); } while (0)
@@ -1285,6 +1332,9 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       bias_s[tid] = epi.bias ? epi.bias[co] : 0.f;
       scale_s[tid] = epi.scale ? epi.scale[co] : 1.f;
     }
+    int* ready = reinterpret_cast<int*>(smem + C::CTR);
+    int* retired = ready + 2;
+    if (!PERSIST && TLOD_WS_FLAGS && tid < 4) ready[tid] = tid < 2 ? 4 : 0;
 #pragma unroll
     for (int i = 0; i < RB; ++i)
 #pragma unroll
@@ -1294,6 +1344,55 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     WS_STAMP(8);
     int c = it.c_begin;
     const int c_end = it.c_end;
+    if constexpr (!PERSIST && TLOD_WS_FLAGS) {
+      // relative chunk j lives in buffer j & 1 as its (j >> 1)-th use: ready when the
+      // buffer's count reaches 4 ((j >> 1) + 1) (four producer waves), retired by the eight
+      // MFMA waves' adds
+      auto wait_ready = [&](int j) {
+        WS_STAMP(0);
+        ws_wait_ge(&ready[j & 1], 4 * ((j >> 1) + 1));
+        WS_STAMP(1);
+      };
+      auto retire = [&](int j) { ws_signal(&retired[j & 1]); };
+      int j = 0;
+      for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4, j += 4) {
+        wait_ready(j);
+        step16(aoff_s(0), boff_s(0));
+        step16(aoff_s(1), boff_s(1));
+        wait_ready(j + 1);
+        step16(aoff_s(2), boff_s(2));
+        retire(j);
+        step16(aoff_s(3), boff_s(3));
+        wait_ready(j + 2);
+        step16(aoff_s(4), boff_s(4));
+        retire(j + 1);
+        step16(aoff_s(5), boff_s(5));
+        wait_ready(j + 3);
+        step16(aoff_s(6), boff_s(6));
+        retire(j + 2);
+        step16(aoff_s(7), boff_s(7));
+        step16(aoff_s(8), boff_s(8));
+        retire(j + 3);
+      }
+      for (; c + 1 < c_end; c += 2, j += 2) {
+        wait_ready(j);
+        step16(aoff_s(0), boff_s(0));
+        step16(aoff_s(1), boff_s(1));
+        wait_ready(j + 1);
+        step16(aoff_s(2), boff_s(2));
+        retire(j);
+        step16(aoff_s(3), boff_s(3));
+        step8(aoff4, boff4);
+        retire(j + 1);
+      }
+      if (c < c_end) {
+        wait_ready(j);
+        step16(aoff_s(0), boff_s(0));
+        step16(aoff_s(1), boff_s(1));
+        step8(aoffL, boffL);
+      }
+      c = c_end;
+    }
     // Four chunks (36 (tap, 8-channel) units) are nine 16x16x32 k-steps; a chunk pair's 18
     // units leave a 16x16x16 step, which issues at the 16x16x32's 16 cycles for half the
     // work (tools/probe/mfma_rate.hip), so whole frames run first.  Steps 2, 4 and 6 read
@@ -2311,7 +2410,8 @@ static bool use_band(int H, int W) {
 static bool use_ws(int Cin, int H, int W) {
   static const bool ws = tune_knob("TLOD_CONV_WS", 1) != 0;
   static const int min_cin = tune_knob("TLOD_WS_MINCIN", 128);
-  return ws && Cin >= min_cin && (TLOD_WS_FLAT != 0 || (size_t)Cin * H * W * 4 < (1ull << 31));
+  // raw buffer loads: 32-bit byte offsets into one image (+ 8 channels of headroom)
+  return ws && Cin >= min_cin && (size_t)(Cin + 8) * H * W * 4 < (1ull << 31);
 }
 
 // Tile of the warp-specialized kernel for an H x W map: the fewest tiles of TH x TW <= 512
