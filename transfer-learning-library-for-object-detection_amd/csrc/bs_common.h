@@ -132,6 +132,9 @@ __device__ f32x4v raw_buffer_load_v4f32(i32x4 rsrc, int voffset, int soffset, in
     __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 __device__ float raw_buffer_load_f32(i32x4 rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.f32");
+// (a store at an offset past the range — kBufOOB — is dropped by the hardware)
+__device__ void raw_buffer_store_f32(float v, i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.f32");
 
 __device__ __forceinline__ i32x4 make_buffer_rsrc(const void* p, unsigned bytes) {
   struct __attribute__((packed)) R {

@@ -842,7 +842,8 @@ struct WsCfg : BsCfg<WM, WN, MI, NJ, NP, false> {
   static constexpr int B_PLANE = BPOS * 16;
   static constexpr int BUF0 = B::NPL * (A_PLANE + B_PLANE);
   static constexpr int BUF = (BUF0 / 16) % 2 == 0 ? BUF0 + 16 : BUF0;
-  static constexpr int CTR = 2 * BUF + 4 * B::BM * 4;  // ready[2], retired[2] (TLOD_WS_FLAGS)
+  static constexpr int AUX = 2 * BUF;                 // (bias, scale) slots of two items
+  static constexpr int CTR = AUX + 4 * B::BM * 4;  // ready[2], retired[2] (TLOD_WS_FLAGS)
   static constexpr int LDS_BYTES = CTR + 16;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
@@ -1325,7 +1326,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
   int k = 0;
   for (; k < n_mine; ++k) {
     const WsItem it = item(vidx(k));
-    float* bias_s = reinterpret_cast<float*>(smem + 2 * C::BUF) + (k & 1) * 2 * C::BM;
+    float* bias_s = reinterpret_cast<float*>(smem + C::AUX) + (k & 1) * 2 * C::BM;
     float* scale_s = bias_s + C::BM;
     if (tid < C::BM) {
       const int co = min(it.m0 + tid, Cout - 1);
@@ -1496,66 +1497,60 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
       }
     }
     if (!pooled) {
-      float* Yn = Y + (size_t)it.n * Cout * HWi;
-      const float* Rn = epi.residual ? epi.residual + (size_t)it.n * Cout * HWi : nullptr;
-      const float* Mn = epi.mask ? epi.mask + (size_t)it.n * Cout * HWi : nullptr;
-      int pix[CB];  // -1: outside the tile / map
+      // Branch-free: 32-bit offsets into the image's planes through buffer resources; an
+      // element outside the tile / map / Cout gets offset kBufOOB, which the hardware drops
+      // (store) or reads as 0 (residual / mask load).  The per-element bounds checks and
+      // 64-bit addresses of a plain store epilogue compiled to ~10 branchy instructions per
+      // element: 29k of a tile's 317k cycles with the stores themselves removed (round 4).
+      const size_t img_off = (size_t)it.n * Cout * HWi;
+      const unsigned plane_bytes = (unsigned)Cout * HWi * 4u;
+      const i32x4 y_rsrc = make_buffer_rsrc(Y + img_off, plane_bytes);
+      const float* Rn = epi.residual ? epi.residual + img_off : nullptr;
+      const float* Mn = epi.mask ? epi.mask + img_off : nullptr;
+      const i32x4 r_rsrc = make_buffer_rsrc(Rn ? Rn : Y, Rn ? plane_bytes : 0u);
+      const i32x4 m_rsrc = make_buffer_rsrc(Mn ? Mn : Y, Mn ? plane_bytes : 0u);
+      int pixo[CB];  // byte offset of the lane's pixel in a channel plane (-1: none)
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
         const int q = wn * 64 + cb * 16 + l16;
         const int h = it.h0 + q / TW, w = it.w0 + q % TW;
-        pix[cb] = q < TH * TW && h < H && w < W ? h * W + w : -1;
+        pixo[cb] = q < TH * TW && h < H && w < W ? (h * W + w) * 4 : -1;
       }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
-        // residual / mask operands of this row block loaded together, ahead of its stores
-        // (interleaved with the stores they would each pay a full load latency: the
-        // compiler cannot move a load above a store that may alias it)
-        float ext[CB][4];
+        int off[CB][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
+          const int rowo = co < Cout ? co * HWi * 4 : -1;
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) off[cb][r] = (rowo | pixo[cb]) >= 0 ? rowo + pixo[cb] : kBufOOB;
+        }
+        // residual / mask operands of the row block loaded together, ahead of its stores
+        float ext[CB][4], msk[CB][4];
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
-            const size_t idx = (size_t)co * HWi + pix[cb];
-            const bool ok = pix[cb] >= 0 && co < Cout;
-            ext[cb][r] = Rn ? (ok ? Rn[idx] : 0.f) : Mn ? (ok ? Mn[idx] : 0.f) : 0.f;
+            ext[cb][r] = Rn ? raw_buffer_load_f32(r_rsrc, off[cb][r], 0, 0) : 0.f;
+            msk[cb][r] = Mn ? raw_buffer_load_f32(m_rsrc, off[cb][r], 0, 0) : 1.f;
           }
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          if (pix[cb] < 0) continue;
+        for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
-            const int co = it.m0 + ml;
-            if (co < Cout) {
-              const size_t idx = (size_t)co * HWi + pix[cb];
-              float val = acc[rb][cb][r];
-              if (has_scale) val *= scale_s[ml];
-              val += bias_s[ml];
-              if (Rn) val += ext[cb][r];
-              if (epi.relu) val = fmaxf(val, 0.f);
-              if (Mn && !Rn && !(ext[cb][r] > 0.f)) val = 0.f;
-#if TLOD_WS_NOSTORE  // timing-only diagnostic build: the epilogue's stores skipped
-              if (val == 1234.5678f)
+            float val = acc[rb][cb][r];
+            if (has_scale) val *= scale_s[ml];
+            val += bias_s[ml];
+            if (Rn) val += ext[cb][r];
+            if (epi.relu) val = fmaxf(val, 0.f);
+            if (Mn && !(msk[cb][r] > 0.f)) val = 0.f;
+#if TLOD_WS_NOSTORE  // timing-only diagnostic build: the epilogue's stores dropped
+            off[cb][r] = kBufOOB;
 #endif
-              Yn[idx] = val;
-            }
+            raw_buffer_store_f32(val, y_rsrc, off[cb][r], 0, 0);
           }
-        }
-      }
-      if (Rn && Mn) {  // both (not produced by the library's callers): mask in a second pass
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-          for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
-              if (pix[cb] < 0 || co >= Cout) continue;
-              const size_t idx = (size_t)co * HWi + pix[cb];
-              if (!(Mn[idx] > 0.f)) Yn[idx] = 0.f;
-            }
       }
     }
     WS_STAMP(9);
@@ -2407,11 +2402,11 @@ static bool use_band(int H, int W) {
 // per tile: the per-tile prologue dominates).  TLOD_CONV_WS=0 disables it.
 // One predicate for the plan (resident slots) and the launch.  Only the raw-buffer-load
 // build (TLOD_WS_FLAT == 0) has 32-bit offsets into one image.
-static bool use_ws(int Cin, int H, int W) {
+static bool use_ws(int Cin, int Cout, int H, int W) {
   static const bool ws = tune_knob("TLOD_CONV_WS", 1) != 0;
   static const int min_cin = tune_knob("TLOD_WS_MINCIN", 128);
-  // raw buffer loads: 32-bit byte offsets into one image (+ 8 channels of headroom)
-  return ws && Cin >= min_cin && (size_t)(Cin + 8) * H * W * 4 < (1ull << 31);
+  // raw buffer loads / stores: 32-bit byte offsets into one image (+ 8 channels of headroom)
+  return ws && Cin >= min_cin && (size_t)(std::max(Cin, Cout) + 8) * H * W * 4 < (1ull << 31);
 }
 
 // Tile of the warp-specialized kernel for an H x W map: the fewest tiles of TH x TW <= 512
@@ -2458,7 +2453,7 @@ static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_sp
   WsTile wt{C::TH, C::TW};
   bool ws = false;
   if constexpr (!BAND)
-    if (use_ws(Cin, H, W)) {
+    if (use_ws(Cin, Cout, H, W)) {
       ws = true;
       slots = ws_slots<WM, WN, MI, NJ, NP>();
       wt = ws_tile(H, W, !allow_split);  // allow_split == false: the pooling epilogue
@@ -2494,7 +2489,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
   bool launched = false;
   if constexpr (!BAND) {
     // warp-specialized kernel (persistent: at most one workgroup per slot)
-    if (use_ws(Cin, H, W)) {
+    if (use_ws(Cin, Cout, H, W)) {
       using WC = WsCfg<WM, WN, MI, NJ, NP>;
       // persistent (TLOD_WS_PERSIST=1) or one work item per workgroup (default: measured
       // faster — an exiting workgroup's output stores drain while the next one stages)
@@ -2561,7 +2556,7 @@ static int conv_fwd_bs_dispatch(const float* X, const unsigned short* Wp, Epi ep
   } while (0)
   // pooling: 2D tiles; the warp-specialized kernel's flexible tiles replace band tiles
   const bool band = use_band(H, W) && epi.pool == nullptr &&
-                    !(use_ws(Cin, H, W) && tune_knob("TLOD_WS_FLEX", 1) != 0);
+                    !(use_ws(Cin, Cout, H, W) && tune_knob("TLOD_WS_FLEX", 1) != 0);
   if (nprod == 6 && band) TLOD_BS_CFG(1, 8, 2, 2, 6, true);
   if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6, false);
   if (band) TLOD_BS_CFG(1, 8, 2, 2, 3, true);
