@@ -56,21 +56,37 @@ def parse():
 
 
 def conv_bytes(kind, shape):
-    """Algorithmic HBM bytes of one conv launch: each operand read once, the result written
-    once (fp32).  shape = (N, Cin, H, W, Cout, KS) of the forward convolution."""
+    """Algorithmic HBM bytes of one launch: each operand read once, the result written once
+    (fp32).  Convs: shape = (N, Cin, H, W, Cout, KS) of the forward convolution; GEMMs
+    (tlod.linear): shape = (M, N, K)."""
+    if kind.startswith("gemm"):
+        M, N, K = shape
+        return 4 * (M * K + N * K + M * N)
     N, Cin, H, W, Cout, KS = shape
     x, y, w = N * Cin * H * W * 4, N * Cout * H * W * 4, Cout * Cin * KS * KS * 4
     return x + y + w  # fwd: X, W -> Y; dgrad: dY, W -> dX; wgrad: dY, X -> dW
 
 
+def family(kind, shape):
+    """Kernel family of a timed launch: (op, arithmetic) — op conv3x3 (the patch-staged and
+    warp-specialized kernels), conv1x1 (the per-image conv GEMM) or gemm (tlod.linear's
+    fc / RoI-head GEMMs)."""
+    math = kind.split("/")[1]
+    if kind.startswith("gemm"):
+        return "gemm/" + math
+    return ("conv3x3/" if shape[5] == 3 else "conv1x1/") + math
+
+
 def conv_roofline(records):
-    """Aggregate the timed conv launches: algorithmic FLOPs / measured kernel time."""
-    tot_f, tot_ms, by, shapes = 0.0, 0.0, {}, {}
+    """Aggregate the timed conv and GEMM launches: algorithmic FLOPs / measured kernel time,
+    per kind and per family; the dominant family is the one with the most time."""
+    tot_f, tot_ms, by, shapes, fam = 0.0, 0.0, {}, {}, {}
     for s, e, flops, kind, shape in records:
         ms = s.elapsed_time(e)
         tot_f += flops
         tot_ms += ms
-        for key, table in ((kind, by), ((kind,) + tuple(shape), shapes)):
+        for key, table in ((kind, by), ((kind,) + tuple(shape), shapes),
+                           (family(kind, shape), fam)):
             d = table.setdefault(key, [0.0, 0.0, 0, 0.0])
             d[0] += flops
             d[1] += ms
@@ -78,26 +94,25 @@ def conv_roofline(records):
             d[3] += conv_bytes(kind, shape)
     if os.environ.get("TLOD_BENCH_SHAPES"):
         for k, v in sorted(shapes.items(), key=lambda kv: -kv[1][1]):
-            print(f"{k[0]:6s} N={k[1]} Cin={k[2]:4d} {k[3]:4d}x{k[4]:<4d} Cout={k[5]:4d} KS={k[6]} "
-                  f"launches={v[2]:4d} ms={v[1]:8.3f} TF={v[0] / (v[1] * 1e-3) / 1e12:7.2f}",
-                  file=sys.stderr)
+            print(f"{k[0]:12s} {k[1:]} launches={v[2]:4d} ms={v[1]:8.3f} "
+                  f"TF={v[0] / (v[1] * 1e-3) / 1e12:7.2f}", file=sys.stderr)
     if tot_ms == 0:
-        return 0.0, {}, 0.0, 0.0, 0, None
+        return 0.0, {}, 0.0, 0.0, 0, None, {}
     achieved = tot_f / (tot_ms * 1e-3) / 1e12
     detail = {k: {"launches": v[2], "ms": round(v[1], 3),
                   "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2),
                   "peak": round(PEAKS[k.split("/")[1]], 1)} for k, v in by.items()}
+    fams = {k: {"launches": v[2], "ms": round(v[1], 3),
+                "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2),
+                "frac": round(v[0] / (v[1] * 1e-3) / 1e12 / PEAKS[k.split("/")[1]], 4)}
+            for k, v in fam.items()}
     # the dominant kernel family (most time): its own achieved / peak
-    fam = {}
-    for k, v in by.items():
-        f = fam.setdefault(k.split("/")[1], [0.0, 0.0, 0, 0.0])
-        for i in range(4):
-            f[i] += v[i]
     dom = max(fam, key=lambda m: fam[m][1])
-    dominant = {"math": dom, "achieved": fam[dom][0] / (fam[dom][1] * 1e-3) / 1e12,
-                "peak": PEAKS[dom], "ms": fam[dom][1], "launches": fam[dom][2],
+    dominant = {"family": dom, "math": dom.split("/")[1],
+                "achieved": fam[dom][0] / (fam[dom][1] * 1e-3) / 1e12,
+                "peak": PEAKS[dom.split("/")[1]], "ms": fam[dom][1], "launches": fam[dom][2],
                 "bytes": fam[dom][3]}
-    return achieved, detail, tot_ms, tot_f, len(records), dominant
+    return achieved, detail, tot_ms, tot_f, len(records), dominant, fams
 
 
 def measured_traffic(a):
@@ -134,8 +149,13 @@ def cpu_baseline(steps, H, W, threads):
     threads = max(1, min(threads, avail))
     torch.set_num_threads(threads)
     t = ods.time_cpu_steps(steps, H, W, warmup=2)
-    return {"value": round(1.0 / t, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+    return {"value": round(1.0 / t, 4), "unit": "img/s", "cores": threads,
+            "cores_available": avail,
+            "cores_note": "BASELINE.md §2 asks for all of sched_getaffinity; the GPU box's share "
+                          "of one GPU is 16 host cores, and the oracle step measured slower at "
+                          "64 threads (0.20 img/s) than at 16 (0.36; DESIGN §5), so it runs on "
+                          "min(16, available)",
+            "kind": "port", "cpu_model": cpu_model(),
             "sample": f"2 untimed + {steps} timed DAF-VGG16 steps (1 src + 1 tgt image {H}x{W}, "
                       f"synthetic) of the oracle restatement: numpy RPN/NMS/RoIAlign + torch-CPU "
                       f"fp32 conv/linear, {threads} threads; median s/step = {t:.2f}"}
@@ -192,24 +212,30 @@ def main():
     t1 = time.perf_counter()
     tconv.PROFILE = None
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    per_rank = [float(elapsed.item())]
     if world > 1:
+        gathered = [torch.zeros_like(elapsed) for _ in range(world)]
+        dist.all_gather(gathered, elapsed)
+        per_rank = [float(g.item()) for g in gathered]
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
     ms_per_step = el / a.steps * 1e3
     value = world * a.steps / el  # one source image per rank per step
     last_loss = float(torch.stack(losses).float().mean().item())
 
-    achieved, detail, conv_ms, conv_f, n_launch, dom = conv_roofline(records)
+    achieved, detail, conv_ms, conv_f, n_launch, dom, fams = conv_roofline(records)
     traffic, traffic_src = measured_traffic(a)
-    dom_kernels = ("conv_fwd_bs_kernel", "conv_fwd_bs_ws_kernel", "conv_wgrad_bs_kernel") \
-        if dom["math"] != "f32" else ("conv_fwd_kernel", "conv_wgrad_kernel")
+    fam_kernels = {"conv3x3/bf16x6": ("conv_fwd_bs_kernel", "conv_fwd_bs_ws_kernel",
+                                      "wgrad_ws_kernel"),
+                   "conv3x3/f32": ("conv_fwd_kernel", "conv_wgrad_kernel"),
+                   "conv1x1/bf16x6": ("conv_gemm_bs_kernel", "conv_wgrad_bs_kernel"),
+                   "gemm/bf16x6": ("gemm_bs_kernel",)}
+    dom_kernels = fam_kernels.get(dom["family"], ())
     per_launch_pmc = None
-    if traffic:
+    if traffic and dom_kernels:
         by_k = traffic["bytes_per_step_by_kernel"]
-        # a PMC pass that predates a kernel of the family (e.g. the warp-specialized forward,
-        # on by default since r02's profile) cannot price this run's launches: report none
-        ws_on = dom["math"] != "f32" and os.environ.get("TLOD_CONV_WS", "1") != "0"
-        if not (ws_on and "conv_fwd_bs_ws_kernel" not in by_k):
+        # a PMC pass that predates a kernel of the family cannot price this run's launches
+        if all(k in by_k for k in dom_kernels if k != "conv_fwd_bs_kernel"):
             per_launch_pmc = round(sum(by_k.get(k, 0) for k in dom_kernels) /
                                    (dom["launches"] / a.steps))
     result = {
@@ -238,15 +264,16 @@ def main():
                                      "vs algorithmic bytes per launch (operands read once, "
                                      "result written once)" +
                                      ("" if per_launch_pmc is not None or not traffic else
-                                      "; null: the committed PMC pass predates "
-                                      "conv_fwd_bs_ws_kernel"),
+                                      "; null: the committed PMC pass predates a kernel "
+                                      "of the family"),
                      "traffic_by_kernel_per_step": (traffic or {}).get("bytes_per_step_by_kernel"),
-                     "kernel": f"tlod 3x3/1x1 conv, {dom['math']} arithmetic "
-                               "(the family with the most time in the step)",
+                     "kernel": f"tlod {dom['family']} (the family with the most time of "
+                               "the timed conv + GEMM launches)",
                      "kernel_ms_per_step": round(dom["ms"] / a.steps, 3),
+                     "families": fams,
                      "peak_basis": "f32-equivalent: algorithmic f32 FLOPs at the MFMA peak; "
                                    "bf16xN = 2516.6 TF bf16 dense / N products",
-                     "all_conv": {"achieved": round(achieved, 2), "launches": n_launch,
+                     "all_conv_gemm": {"achieved": round(achieved, 2), "launches": n_launch,
                                   "kernel_ms_per_step": round(conv_ms / a.steps, 3),
                                   "gflop_per_step": round(conv_f / a.steps / 1e9, 2)},
                      "by_kind": detail},
@@ -254,6 +281,9 @@ def main():
                       "1x1 fwd/dgrad": f"{tconv.conv_math()} (>= 64 channels; f32 MFMA for "
                                        "the RPN cls/bbox heads)",
                       "fc6/fc7/DA fc": linear_math()},
+        "rank_ms_per_step": {"min": round(min(per_rank) / a.steps * 1e3, 3),
+                             "max": round(max(per_rank) / a.steps * 1e3, 3),
+                             "spread_pct": round((max(per_rank) / min(per_rank) - 1) * 100, 2)},
         "mean_loss": round(last_loss, 4),
         # ReLU backward passes folded into the next conv's dgrad epilogue, per step (tlod.conv)
         "fused_relu_backward_per_step": {k: v / (a.steps + a.warmup)

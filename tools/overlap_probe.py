@@ -1,0 +1,102 @@
+"""Pre-read of the 8-GPU run on one GPU: when does each gradient bucket become ready during
+the DAF-VGG16 backward, and how much backward time is left to hide its all-reduce?
+
+Records a HIP event when each parameter's gradient lands in the arena (the reducer's
+trigger, tlod.grads.GradArena listeners) and at the end of backward, over a few steps.
+Buckets are cut as tlod.dist.GradBucketReducer cuts them after its first-step relayout
+(gradient-ready order, 32 MB).  An RCCL ring all-reduce of B bytes over n ranks moves
+2 (n - 1) / n x B per GPU; buckets are reduced one after another on the communication
+stream.  The exposed communication at a per-GPU bus bandwidth BW is
+  max(0, end of the last bucket's all-reduce - end of backward)
+and the predicted step = measured 1-GPU step + exposed time.
+usage: python tools/overlap_probe.py [--steps 5] [--bucket-mb 32]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "transfer-learning-library-for-object-detection_amd"))
+
+import torch  # noqa: E402
+
+from tlod.detector.train import SyntheticCityscapes, build_model, make_optimizer, train_step  # noqa: E402
+from tlod.grads import arena_of  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--ranks", type=int, default=8)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    model = build_model("daf", dev, "vgg16")
+    opt = make_optimizer(model, 2e-3, clip=10.0)
+    data = SyntheticCityscapes(dev, H=600, W=1200, seed=1)
+    params = [p for p in model.parameters() if p.requires_grad]
+    arena = arena_of(params[0])
+    marks = []
+    arena.listeners.append(lambda p: marks.append((p, torch.cuda.Event(enable_timing=True))) or
+                           marks[-1][1].record())
+    for _ in range(3):
+        train_step(model, opt, data.next())
+    torch.cuda.synchronize()
+    runs = []
+    for _ in range(a.steps):
+        marks.clear()
+        opt.zero_grad(set_to_none=True)
+        e0, e_fwd, e_bwd, e_end = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+        batch = data.next()
+        e0.record()
+        out = model(*batch)
+        loss = model.total_loss(out, 0.1)
+        e_fwd.record()
+        loss.backward()
+        e_bwd.record()
+        opt.step(grad_scale=1.0)
+        e_end.record()
+        torch.cuda.synchronize()
+        ready = [(p, e_fwd.elapsed_time(ev)) for p, ev in marks]
+        runs.append({"step_ms": e0.elapsed_time(e_end), "fwd_ms": e0.elapsed_time(e_fwd),
+                     "bwd_ms": e_fwd.elapsed_time(e_bwd), "opt_ms": e_bwd.elapsed_time(e_end),
+                     "ready": ready})
+    r = sorted(runs, key=lambda x: x["step_ms"])[len(runs) // 2]  # median step
+    # buckets in gradient-ready order (the reducer's relayout), 32 MB each
+    cap = int(a.bucket_mb * 1024 * 1024 / 4)
+    buckets, cur, cur_n, last_t = [], 0, 0, 0.0
+    for p, t in r["ready"]:
+        n = p.numel()
+        if cur_n and cur_n + n > cap:
+            buckets.append((cur_n * 4, last_t))
+            cur_n = 0
+        cur_n += n
+        last_t = t
+    if cur_n:
+        buckets.append((cur_n * 4, last_t))
+    bwd = r["bwd_ms"]
+    total_bytes = sum(b for b, _ in buckets)
+    n = a.ranks
+    pred = {}
+    for bw in (153.0, 300.0, 600.0, 900.0):  # GB/s per GPU: one xGMI link .. most of seven
+        end = 0.0
+        for b, t in buckets:
+            dur = 2.0 * (n - 1) / n * b / (bw * 1e9) * 1e3 + 0.02  # ms, + 20 us per collective
+            end = max(end, t) + dur
+        exposed = max(0.0, end - bwd)
+        step = r["step_ms"] + exposed
+        pred[f"{int(bw)}GBps"] = {"allreduce_total_ms": round(2.0 * (n - 1) / n * total_bytes / (bw * 1e9) * 1e3, 3),
+                                  "exposed_ms": round(exposed, 3), "step_ms": round(step, 3),
+                                  "img_per_s": round(n * 1e3 / step, 1),
+                                  "efficiency": round(r["step_ms"] / step, 3)}
+    out = {"one_gpu": {k: round(v, 3) for k, v in r.items() if k != "ready"},
+           "gradient_mb": round(total_bytes / 2**20, 1), "buckets": len(buckets),
+           "bucket_ready_ms_after_backward_start": [round(t, 3) for _, t in buckets],
+           "backward_left_after_bucket_ms": [round(bwd - t, 3) for _, t in buckets],
+           "bucket_mb": [round(b / 2**20, 1) for b, _ in buckets],
+           "ranks": n, "prediction": pred}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -28,15 +28,23 @@ PROFILE = None
 
 
 def _timed(kind, shape, fn, math="f32"):
+    """Run one launch; under bench.py's PROFILE also record HIP events around it on the
+    launch stream.  kind: fwd / dgrad / wgrad with shape (N, Cin, H, W, Cout, KS), or
+    gemm (tlod.linear) with shape (M, N, K)."""
     if PROFILE is None:
         return fn()
+    if kind == "gemm":
+        M, Nn, K = shape
+        flops = 2.0 * M * Nn * K
+    else:
+        N, Cin, H, W, Cout, KS = shape
+        flops = 2.0 * N * H * W * Cout * Cin * KS * KS
     kind = f"{kind}/{math}"
-    N, Cin, H, W, Cout, KS = shape
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     r = fn()
     e.record()
-    PROFILE.append((s, e, 2.0 * N * H * W * Cout * Cin * KS * KS, kind, shape))
+    PROFILE.append((s, e, flops, kind, shape))
     return r
 
 

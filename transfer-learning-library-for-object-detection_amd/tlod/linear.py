@@ -43,9 +43,11 @@ def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6", out=None
     ws = _lib.workspace(L.tlod_gemm_bs_workspace_bytes(M, N, K, a_kcontig, b_kcontig, nprod),
                         a.device, "gemm")
     bias = bias.detach().contiguous() if bias is not None else None
-    _lib.check(L.tlod_gemm_bs_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K,
-                                  int(a_kcontig), int(b_kcontig), nprod, _lib.ptr(ws), ws.numel(),
-                                  _lib.stream_of(a)), "gemm_bs")
+    from .conv import _timed  # bench.py's launch timing (tlod.conv.PROFILE), shape (M, N, K)
+    _timed("gemm", (M, N, K), lambda: _lib.check(
+        L.tlod_gemm_bs_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K,
+                           int(a_kcontig), int(b_kcontig), nprod, _lib.ptr(ws), ws.numel(),
+                           _lib.stream_of(a)), "gemm_bs"), math)
     return c
 
 
