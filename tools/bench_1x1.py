@@ -1,0 +1,46 @@
+"""Microbenchmark: the ResNet101 bottleneck 1x1 convs of the DAF-R101 step (2 images,
+600x1200 input: layer1 150x300, layer2 75x150, layer3 38x75) — forward / input gradient on
+the split-bf16 conv GEMM and the weight gradient — split-bf16 TF/s (f32-equivalent)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "transfer-learning-library-for-object-detection_amd"))
+import torch  # noqa: E402
+
+from tlod import conv as tc  # noqa: E402
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+SHAPES = [(256, 64, 150, 300), (64, 256, 150, 300), (512, 128, 75, 150), (128, 512, 75, 150),
+          (1024, 256, 38, 75), (256, 1024, 38, 75)]
+out = {}
+tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+for Cin, Cout, H, W in SHAPES:
+    x = torch.randn(2, Cin, H, W, device="cuda")
+    w = torch.randn(Cout, Cin, 1, 1, device="cuda") * 0.05
+    g = torch.randn(2, Cout, H, W, device="cuda")
+    f = 2.0 * 2 * H * W * Cin * Cout
+    r = {}
+    r["fwd"] = timeit(lambda: tc.conv_fwd(x, w, None, False, math="bf16x6"))
+    r["dgrad"] = timeit(lambda: tc.conv_dgrad(g, w, math="bf16x6"))
+    r["wgrad"] = timeit(lambda: tc.conv_wgrad(g, x, 1, math="bf16x6"))
+    out[f"{Cin}->{Cout}@{H}x{W}"] = {k: {"ms": round(v, 4), "tf": round(f / v / 1e9, 1)}
+                                     for k, v in r.items()}
+    for k in tot:
+        tot[k] += r[k]
+out["total_ms"] = {k: round(v, 4) for k, v in tot.items()}
+print(json.dumps(out))

@@ -25,6 +25,7 @@
 #include "tlod.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace tlod {
 
@@ -32,6 +33,9 @@ namespace {
 
 #ifndef TLOD_MID_STORE
 #define TLOD_MID_STORE 1  // stage the next chunk mid-MFMA-phase (see conv.hip)
+#endif
+#ifndef TLOD_GEMM_DEPTH2  // two chunks of loads in flight (mainloop, MI <= 2 tiles)
+#define TLOD_GEMM_DEPTH2 1
 #endif
 
 constexpr int kBN = 256, kTK = 16, kNT = 512;
@@ -71,8 +75,8 @@ struct Stager {
   int off[IT];     // element offset of this lane's 4-vector at chunk 0 (or -1: dead)
   int lds[IT];     // byte offset inside one plane image (-1: no slot)
   int lim[IT];     // for the tail mask: K - k (KC) or R - r (MN)
-  f32x4v r[IT];
-  unsigned mask[IT];
+  f32x4v r[IT], r2[IT];  // data slots 0 / 1 (mainloop's two-chunk prefetch uses both)
+  unsigned mask[IT], mask2[IT];
 
   __device__ void init(const float* P, int R, int K, int r0, int tid) {
     rsrc = make_buffer_rsrc(P, (unsigned)R * (unsigned)K * 4u);
@@ -93,25 +97,31 @@ struct Stager {
       }
     }
   }
+  template <int S = 0>
   __device__ void load(int kc, int R) {
+    f32x4v* rr = S ? r2 : r;
+    unsigned* mm = S ? mask2 : mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (KC) {
-        r[i] = raw_buffer_load_v4f32(rsrc, off[i] >= 0 ? (off[i] + kc) * 4 : kBufOOB, 0, 0);
-        mask[i] = lt_mask4(lim[i] - kc);
+        rr[i] = raw_buffer_load_v4f32(rsrc, off[i] >= 0 ? (off[i] + kc) * 4 : kBufOOB, 0, 0);
+        mm[i] = lt_mask4(lim[i] - kc);
       } else {  // k rows past K fall past the buffer end (zero)
-        r[i] = raw_buffer_load_v4f32(rsrc, lds[i] >= 0 ? (off[i] + kc * R) * 4 : kBufOOB, 0, 0);
-        mask[i] = lt_mask4(lim[i]);
+        rr[i] = raw_buffer_load_v4f32(rsrc, lds[i] >= 0 ? (off[i] + kc * R) * 4 : kBufOOB, 0, 0);
+        mm[i] = lt_mask4(lim[i]);
       }
     }
   }
+  template <int S = 0>
   __device__ void store(unsigned char* img) const {
+    const f32x4v* rr = S ? r2 : r;
+    const unsigned* mm = S ? mask2 : mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (lds[i] < 0) continue;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ((mask[i] >> e) & 1) ? r[i][e] : 0.f;
+      for (int e = 0; e < 4; ++e) v[e] = ((mm[i] >> e) & 1) ? rr[i][e] : 0.f;
       unsigned sp[3][2];
       split4<NPL>(v, sp);
 #pragma unroll
@@ -210,6 +220,62 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
 #pragma unroll
       for (int r = 0; r < kAccRegs; ++r) acc[i][j][r] = 0.f;
 
+  if constexpr (TLOD_GEMM_DEPTH2 && MI <= 2) {
+    // Two chunks in flight: chunk j of the range sits in data slot j & 1 of the stagers from
+    // its load until its split + store, half way through chunk j - 1's MFMAs; the store then
+    // loads chunk j + 2 into the slot.  Loads and stores are unconditional (a chunk past the
+    // range reads zeros / masked values into the buffer that is not read next), so the loop
+    // body is straight-line and the compiler's vmcnt wait before a store leaves the other
+    // slot's loads in flight (one slot loaded at the top of the iteration gave its loads
+    // half an iteration).  (MI >= 3, the fc GEMMs: spills, no register room.)
+    const int n = c_end - c_begin;
+    sa.template load<0>(c_begin * kTK, Ra);
+    sb.template load<0>(c_begin * kTK, Rb);
+    sa.template load<1>((c_begin + 1) * kTK, Ra);
+    sb.template load<1>((c_begin + 1) * kTK, Rb);
+    sa.template store<0>(smem);
+    sb.template store<0>(smem + NPL * A_PL);
+    sa.template load<0>((c_begin + 2) * kTK, Ra);
+    sb.template load<0>((c_begin + 2) * kTK, Rb);
+    __syncthreads();
+    auto iter = [&](auto slc, int j) {
+      constexpr int S = decltype(slc)::value;  // slot of chunk j + 1
+      const unsigned char* buf = smem + (j & 1) * BUF;
+      unsigned char* nbuf = smem + ((j + 1) & 1) * BUF;
+      auto mid = [&]() {
+        sa.template store<S>(nbuf);
+        sb.template store<S>(nbuf + NPL * A_PL);
+        sa.template load<S>((c_begin + j + 3) * kTK, Ra);
+        sb.template load<S>((c_begin + j + 3) * kTK, Rb);
+      };
+      u32x4 b[kNJ][3];
+#pragma unroll
+      for (int jj = 0; jj < kNJ; ++jj)
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          b[jj][pl] = read_operand<BK>(buf + NPL * A_PL + pl * B_PL, wn * kNJ * 32 + jj * 32, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if (i == MI / 2) mid();
+        u32x4 a[3];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          a[pl] = read_operand<AK>(buf + pl * A_PL, wm * MI * 32 + i * 32, lane);
+#pragma unroll
+        for (int jj = 0; jj < kNJ; ++jj)
+          bs_mac<NP>(acc[i][jj], a[0], a[1], a[2], b[jj][0], b[jj][1], b[jj][2]);
+      }
+      __syncthreads();
+    };
+    const std::integral_constant<int, 0> S0;
+    const std::integral_constant<int, 1> S1;
+    for (int j = 0; j < n; j += 2) {
+      iter(S1, j);  // chunk j from buffer 0; chunk j + 1 (slot 1) -> buffer 1
+      if (j + 1 >= n) break;
+      iter(S0, j + 1);  // chunk j + 1 from buffer 1; chunk j + 2 (slot 0) -> buffer 0
+    }
+    return;
+  }
   auto store = [&](unsigned char* buf) {
     sa.store(buf);
     sb.store(buf + NPL * A_PL);
@@ -502,8 +568,8 @@ struct Im2colStager {
   int xoff, kr, p, c4, h0, w0, C, H, W, P, K;
   bool neg_risk;
   unsigned tmask;
-  f32x4v r[IT];
-  unsigned mask[IT];
+  f32x4v r[IT], r2[IT];  // data slots 0 / 1
+  unsigned mask[IT], mask2[IT];
 
   __device__ void init(const float* X, int N, int C_, int H_, int W_, int img, int p0, int tid) {
     C = C_; H = H_; W = W_; P = H * W; K = C * 9;
@@ -519,7 +585,10 @@ struct Im2colStager {
     // a tap vector can start before the tensor only in image 0's first row band
     neg_risk = img == 0 && p0 <= W;
   }
+  template <int S = 0>
   __device__ void load(int kc, int) {
+    f32x4v* r = S ? this->r2 : this->r;
+    unsigned* mask = S ? this->mask2 : this->mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int k = kc + kr + 8 * i;
@@ -555,7 +624,10 @@ struct Im2colStager {
       }
     }
   }
+  template <int S = 0>
   __device__ void store(unsigned char* img) const {
+    const f32x4v* r = S ? this->r2 : this->r;
+    const unsigned* mask = S ? this->mask2 : this->mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       float v[4];
