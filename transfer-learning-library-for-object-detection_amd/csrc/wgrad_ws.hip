@@ -67,6 +67,9 @@ static_assert(A_ITEMS % (NPW * 64) == 0, "A staging");
 #ifndef TLOD_WGWS_BSPLIT  // 1: the MFMA waves stage B (the X patch), the producers only A
 #define TLOD_WGWS_BSPLIT 1
 #endif
+#ifndef TLOD_WGWS_KSUM  // per-k-step sums of the cross products (accuracy; see the k-step)
+#define TLOD_WGWS_KSUM 0
+#endif
 #ifndef TLOD_WGWS_PRIO  // s_setprio of the producer waves (0: default)
 #define TLOD_WGWS_PRIO 0
 #endif
@@ -373,18 +376,31 @@ wgrad_ws_kernel(const float* __restrict__ G, const float* __restrict__ X,
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        acc[i][t] = wgws_mfma(a[i][0], b[0], acc[i][t]);
-        acc[i][t] = wgws_mfma(a[i][1], b[0], acc[i][t]);
-        acc[i][t] = wgws_mfma(a[i][0], b[1], acc[i][t]);
-        acc[i][t] = wgws_mfma(a[i][2], b[0], acc[i][t]);
-        acc[i][t] = wgws_mfma(a[i][1], b[1], acc[i][t]);
-        acc[i][t] = wgws_mfma(a[i][0], b[2], acc[i][t]);
+        if (TLOD_WGWS_KSUM) {
+          // the k-step's five cross products summed from zero, then the f32 add of that
+          // sum after hi*hi: the small products are not floored against the running
+          // accumulator (bs_common.h bs_mac)
+          f32x4 x = wgws_mfma(a[i][1], b[0], f32x4{0.f, 0.f, 0.f, 0.f});
+          x = wgws_mfma(a[i][0], b[1], x);
+          x = wgws_mfma(a[i][2], b[0], x);
+          x = wgws_mfma(a[i][1], b[1], x);
+          x = wgws_mfma(a[i][0], b[2], x);
+          acc[i][t] = wgws_mfma(a[i][0], b[0], acc[i][t]) + x;
+        } else {
+          acc[i][t] = wgws_mfma(a[i][0], b[0], acc[i][t]);
+          acc[i][t] = wgws_mfma(a[i][1], b[0], acc[i][t]);
+          acc[i][t] = wgws_mfma(a[i][0], b[1], acc[i][t]);
+          acc[i][t] = wgws_mfma(a[i][2], b[0], acc[i][t]);
+          acc[i][t] = wgws_mfma(a[i][1], b[1], acc[i][t]);
+          acc[i][t] = wgws_mfma(a[i][0], b[2], acc[i][t]);
+        }
       }
     }
   };
   // B staging by the MFMA waves (TLOD_WGWS_BSPLIT): lane tid < 432 owns one (octet,
   // position) item of the patch; chunk j's 8 channel values are loaded two chunks ahead
   // into register slot j & 1 and split + stored between the two k-steps of chunk j - 1
+  // (items spread evenly over the 8 waves, 54 lanes each, measured 1% slower)
   const bool b_item = TLOD_WGWS_BSPLIT && tid < B_ITEMS;
   const int b_oct = tid / PP, b_pos = tid % PP;
   const int b_lds = b_oct * B_OCT + b_pos * 16;
@@ -486,8 +502,19 @@ __global__ void __launch_bounds__(256) wgws_reduce_kernel(const float* __restric
   if (idx >= tiles * TILE_FLOATS / 4) return;
   const size_t stride4 = (size_t)tiles * TILE_FLOATS / 4;
   const f32x4* s4 = reinterpret_cast<const f32x4*>(slab) + idx;
+  // split order kept (deterministic); four loads in flight per group (the loop issued one
+  // load per dependent add: latency-bound)
   f32x4 sum = s4[0];
-  for (int k = 1; k < splits; ++k) sum += s4[k * stride4];
+  int k = 1;
+  for (; k + 4 <= splits; k += 4) {
+    const f32x4 v0 = s4[k * stride4], v1 = s4[(k + 1) * stride4];
+    const f32x4 v2 = s4[(k + 2) * stride4], v3 = s4[(k + 3) * stride4];
+    sum += v0;
+    sum += v1;
+    sum += v2;
+    sum += v3;
+  }
+  for (; k < splits; ++k) sum += s4[k * stride4];
   int r = idx;
   const int lane = r % 64; r /= 64;
   const int t = r % 9; r /= 9;
