@@ -28,7 +28,7 @@ def timeit(fn, iters=20, warmup=3):
 SHAPES = [(256, 64, 150, 300), (64, 256, 150, 300), (512, 128, 75, 150), (128, 512, 75, 150),
           (1024, 256, 38, 75), (256, 1024, 38, 75)]
 out = {}
-tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+tot = {"fwd": 0.0, "fwd_res": 0.0, "dgrad": 0.0, "wgrad": 0.0}
 for Cin, Cout, H, W in SHAPES:
     x = torch.randn(2, Cin, H, W, device="cuda")
     w = torch.randn(Cout, Cin, 1, 1, device="cuda") * 0.05
@@ -36,6 +36,11 @@ for Cin, Cout, H, W in SHAPES:
     f = 2.0 * 2 * H * W * Cin * Cout
     r = {}
     r["fwd"] = timeit(lambda: tc.conv_fwd(x, w, None, False, math="bf16x6"))
+    # the bottleneck conv3 / downsample form: folded BN scale + shift, residual, ReLU
+    sc = torch.rand(Cout, device="cuda") + 0.5
+    sh = torch.randn(Cout, device="cuda")
+    res = torch.randn(2, Cout, H, W, device="cuda")
+    r["fwd_res"] = timeit(lambda: tc.conv_fwd(x, w, sh, True, scale=sc, residual=res, math="bf16x6"))
     r["dgrad"] = timeit(lambda: tc.conv_dgrad(g, w, math="bf16x6"))
     r["wgrad"] = timeit(lambda: tc.conv_wgrad(g, x, 1, math="bf16x6"))
     out[f"{Cin}->{Cout}@{H}x{W}"] = {k: {"ms": round(v, 4), "tf": round(f / v / 1e9, 1)}

@@ -2045,6 +2045,8 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
     float4 s = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // unrolled: eight split loads in flight, the adds still in split order
+#pragma unroll 8
     for (int k = 0; k < splits; ++k) {
       const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * count)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -2630,7 +2632,7 @@ static int wgrad_splits(int N, int Cin, int H, int W, int Cout, int KS) {
 // (sp writes + sp reads + 1 write of Cout*Ktot floats).  Small maps (conv5 / RPN at
 // 37x75) cannot afford the 16-64 splits that fill the chip on conv3.
 static int pick_splits_cost(long long tiles, int chunks, int slots, double chunk_s,
-                            double dw_bytes) {
+                            double dw_bytes, double* t_out = nullptr) {
   int best = 1;
   double best_t = 1e30;
   const int smax = std::max(1, std::min(128, chunks / 4));
@@ -2644,20 +2646,23 @@ static int pick_splits_cost(long long tiles, int chunks, int slots, double chunk
       best = esp;
     }
   }
+  if (t_out) *t_out = best_t;
   return best;
 }
 
 template <int WM, int WN, int MI, int NJ, int KS, int NP>
 struct WgradBs {
   using C = WgBsCfg<WM, WN, MI, NJ, NP>;
-  static int splits(int N, int Cin, int H, int W, int Cout) {
+  static int splits(int N, int Cin, int H, int W, int Cout, double* t_out = nullptr) {
     static const int slots =
         resident_slots(conv_wgrad_bs_kernel<WM, WN, MI, NJ, KS, NP>, C::NT, C::LDS_BYTES);
     const long long tiles = (long long)div_up(Cout, C::BM) * div_up(Cin * KS * KS, C::BN);
     const int chunks = N * div_up(H * W, C::TK);
-    // bf16 MFMA time of one chunk per resident slot at ~50% of the dense peak
-    const double chunk_s = 2.0 * C::BM * C::BN * C::TK * NP / (2516.6e12 * 0.5 / slots);
-    return pick_splits_cost(tiles, chunks, slots, chunk_s, 4.0 * Cout * Cin * KS * KS);
+    // bf16 MFMA time of one chunk per resident slot at ~50% of the dense peak (a 128 x 128
+    // tile reads twice the LDS bytes per MFMA of a 256 x 256 one: ~40%)
+    const double eff = C::BM * C::BN >= 256 * 256 ? 0.5 : 0.4;
+    const double chunk_s = 2.0 * C::BM * C::BN * C::TK * NP / (2516.6e12 * eff / slots);
+    return pick_splits_cost(tiles, chunks, slots, chunk_s, 4.0 * Cout * Cin * KS * KS, t_out);
   }
   static int launch(const float* G, const float* X, float* slab, float* db_slab, int splits,
                     int N, int Cin, int H, int W, int Cout, hipStream_t s) {
@@ -2679,12 +2684,38 @@ struct WgradBs {
   }
 };
 
+// 1x1 weight gradients have small outputs (Cout x Cin) over long K (all pixels), so the
+// 256 x 256 tiles leave a handful of tiles that must be split many ways over the pixels, each
+// split writing a full dW slab: 256 -> 1024 at 38x75 ran 4 tiles x 64 splits (64 MB of
+// slabs).  128 x 128 tiles give 4x the tiles for 1/4 of the slab traffic at a lower MFMA
+// efficiency; the cost model picks (TLOD_WG1X1_TILE = 256 / 128 forces one).
+static bool wgrad1x1_small_tile(int N, int Cin, int H, int W, int Cout, int nprod) {
+  static const int force = [] {
+    const char* e = getenv("TLOD_WG1X1_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 256) return false;
+  if (force == 128) return true;
+  double t_big = 0, t_small = 0;
+  if (nprod == 6) {
+    WgradBs<2, 4, 4, 2, 1, 6>::splits(N, Cin, H, W, Cout, &t_big);
+    WgradBs<2, 4, 2, 1, 1, 6>::splits(N, Cin, H, W, Cout, &t_small);
+  } else {
+    WgradBs<2, 4, 4, 2, 1, 3>::splits(N, Cin, H, W, Cout, &t_big);
+    WgradBs<2, 4, 2, 1, 1, 3>::splits(N, Cin, H, W, Cout, &t_small);
+  }
+  return t_small < t_big;
+}
+
 template <typename F>
-static int with_wgrad_bs_cfg(int KS, int nprod, F&& f) {
+static int with_wgrad_bs_cfg(int N, int Cin, int H, int W, int Cout, int KS, int nprod, F&& f) {
   if (KS == 3 && nprod == 6) return f(WgradBs<2, 4, 4, 2, 3, 6>{});
   if (KS == 3 && nprod == 3) return f(WgradBs<2, 4, 4, 2, 3, 3>{});
-  if (KS == 1 && nprod == 6) return f(WgradBs<2, 4, 4, 2, 1, 6>{});
-  if (KS == 1 && nprod == 3) return f(WgradBs<2, 4, 4, 2, 1, 3>{});
+  if (KS == 1) {
+    const bool small = wgrad1x1_small_tile(N, Cin, H, W, Cout, nprod);
+    if (nprod == 6) return small ? f(WgradBs<2, 4, 2, 1, 1, 6>{}) : f(WgradBs<2, 4, 4, 2, 1, 6>{});
+    if (nprod == 3) return small ? f(WgradBs<2, 4, 2, 1, 1, 3>{}) : f(WgradBs<2, 4, 4, 2, 1, 3>{});
+  }
   return -1;
 }
 
@@ -2827,7 +2858,7 @@ int launch_db_reduce(const float* db_slab, int splits, int C, float* db, int acc
 extern "C" size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
                                                      int nprod) {
   if (wgrad_ws_applies(N, Cin, H, W, Cout, KS, nprod)) return wgrad_ws_workspace(N, Cin, H, W, Cout);
-  const int sp = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
+  const int sp = with_wgrad_bs_cfg(N, Cin, H, W, Cout, KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
   return sp > 0 ? wgrad_bs_ws(sp, Cin, Cout, KS) : 0;
 }
 
@@ -2846,7 +2877,7 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
   if (wgrad_ws_applies(N, Cin, H, W, Cout, KS, nprod))
     return wgrad_ws_launch(dy, x, dw, db, accumulate, N, Cin, H, W, Cout, ws, ws_bytes, s);
   const int splits =
-      with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
+      with_wgrad_bs_cfg(N, Cin, H, W, Cout, KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
   if (ws_bytes < wgrad_bs_ws(splits, Cin, Cout, KS)) {
     set_error("tlod_conv_wgrad_bs_f32: workspace too small");
     return kWorkspace;
@@ -2856,7 +2887,7 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
                                                  align_up((size_t)splits * Cout * Cin * KS * KS *
                                                               sizeof(float), 16))
                       : nullptr;
-  const int st = with_wgrad_bs_cfg(KS, nprod, [&](auto cfg) {
+  const int st = with_wgrad_bs_cfg(N, Cin, H, W, Cout, KS, nprod, [&](auto cfg) {
     return cfg.launch(dy, x, slab, db_slab, splits, N, Cin, H, W, Cout, s);
   });
   if (st) return st;

@@ -694,37 +694,61 @@ conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, C
   }
   auto& acc = acc_.t;
 
-  // epilogue, one output channel (i, r) at a time: its scale / bias loaded once for the
-  // lane's kNJ pixels
   const size_t ybase = (size_t)img * Cout * P;
-  float* St = slab + ((size_t)split * n_tail + ti) * BM * kBN;
   const int nl0 = wn * kNJ * 32;
+  if (!direct) {  // tile-local slab, reduced by conv_tail_reduce_kernel
+    float* St = slab + ((size_t)split * n_tail + ti) * BM * kBN;
 #pragma unroll
-  for (int i = 0; i < acc_rows<MI>(); ++i)
+    for (int i = 0; i < acc_rows<MI>(); ++i)
+#pragma unroll
+      for (int r = 0; r < kAccRegs; ++r)
+#pragma unroll
+        for (int j = 0; j < kAccCols; ++j)
+          St[(wm * MI * 32 + acc_row(i, r, lane)) * kBN + nl0 + acc_col(j, lane)] = acc[i][j][r];
+    return;
+  }
+  // Direct epilogue, branch-free: elements outside the map / Cout get an out-of-range buffer
+  // offset (their residual loads read 0, their stores are dropped).  The residual operands
+  // of one accumulator row block are loaded together ahead of its stores — loaded one by one
+  // between the stores, every load paid a full memory latency (256 -> 1024 at 38x75 with a
+  // residual: 67 us per launch).
+  const i32x4 y_rsrc = make_buffer_rsrc(Y + ybase, (unsigned)Cout * (unsigned)P * 4u);
+  const i32x4 r_rsrc = make_buffer_rsrc(epi.residual ? epi.residual + ybase : Y + ybase,
+                                        epi.residual ? (unsigned)Cout * (unsigned)P * 4u : 0u);
+  int pix4[kAccCols];
+#pragma unroll
+  for (int j = 0; j < kAccCols; ++j) {
+    const int pix = p0 + nl0 + acc_col(j, lane);
+    pix4[j] = pix < P ? pix * 4 : kBufOOB;
+  }
+#pragma unroll
+  for (int i = 0; i < acc_rows<MI>(); ++i) {
+    float res[kAccRegs][kAccCols];
+    if (epi.residual) {
+#pragma unroll
+      for (int r = 0; r < kAccRegs; ++r) {
+        const int co = m0 + wm * MI * 32 + acc_row(i, r, lane);
+#pragma unroll
+        for (int j = 0; j < kAccCols; ++j)
+          res[r][j] = raw_buffer_load_f32(r_rsrc, co < Cout && pix4[j] != kBufOOB ? co * P * 4 + pix4[j] : kBufOOB, 0, 0);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < kAccRegs; ++r) {
-      const int ml = wm * MI * 32 + acc_row(i, r, lane);
-      const int co = m0 + ml;
-      if (!direct) {  // tile-local slab, reduced by conv_tail_reduce_kernel
-#pragma unroll
-        for (int j = 0; j < kAccCols; ++j) St[ml * kBN + nl0 + acc_col(j, lane)] = acc[i][j][r];
-        continue;
-      }
-      if (co >= Cout) continue;
-      const float sc = epi.scale ? epi.scale[co] : 1.f, bi = epi.bias ? epi.bias[co] : 0.f;
+      const int co = m0 + wm * MI * 32 + acc_row(i, r, lane);
+      const int cc = min(co, Cout - 1);
+      const float sc = epi.scale ? epi.scale[cc] : 1.f, bi = epi.bias ? epi.bias[cc] : 0.f;
 #pragma unroll
       for (int j = 0; j < kAccCols; ++j) {
-        const int pix = p0 + nl0 + acc_col(j, lane);
-        if (pix >= P) continue;
-        const size_t idx = ybase + (size_t)co * P + pix;
         float v = acc[i][j][r];
         if (epi.scale) v *= sc;
         v += bi;
-        if (epi.residual) v += epi.residual[idx];
+        if (epi.residual) v += res[r][j];
         if (epi.relu) v = fmaxf(v, 0.f);
-        Y[idx] = v;
+        raw_buffer_store_f32(v, y_rsrc, co < Cout && pix4[j] != kBufOOB ? co * P * 4 + pix4[j] : kBufOOB, 0, 0);
       }
     }
+  }
 }
 
 // Tail tiles: Y = act(sum_s slab[s][tile] * scale + bias + residual), fixed split order.
@@ -847,6 +871,24 @@ auto with_conv1x1_gemm(int w_layout, int nprod, int N, int H, int W, int Cout, F
 
 }  // namespace
 
+// gemm_ws.hip: the warp-specialized form (bf16x6)
+bool gemm_ws_applies(int M, int N, int K, int nprod);
+size_t gemm_ws_workspace(int M, int N, int K);
+int gemm_ws_launch(const float* a, const float* b, const float* bias, const float* res, int relu,
+                   float* c, int M, int N, int K, int a_kcontig, int b_kcontig, void* ws,
+                   size_t ws_bytes, hipStream_t s);
+
+// c = act(c + residual) in place (the epilogue of gemm_bs_kernel's callers of the _ex form)
+__global__ void gemm_res_act_kernel(float* __restrict__ c, const float* __restrict__ res, int relu,
+                                    size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float v = c[i];
+    if (res) v += res[i];
+    if (relu) v = fmaxf(v, 0.f);
+    c[i] = v;
+  }
+}
+
 }  // namespace tlod
 
 using namespace tlod;
@@ -854,6 +896,7 @@ using namespace tlod;
 extern "C" size_t tlod_gemm_bs_workspace_bytes(int M, int N, int K, int a_kcontig, int b_kcontig,
                                                int nprod) {
   if (M <= 0 || N <= 0 || K <= 0 || (nprod != 3 && nprod != 6)) return 0;
+  if (gemm_ws_applies(M, N, K, nprod)) return gemm_ws_workspace(M, N, K);
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod,
                    [&](auto g) { return g.ws_bytes(M, N, K); });
 }
@@ -865,9 +908,34 @@ extern "C" int tlod_gemm_bs_f32(const float* a, const float* b, const float* bia
   TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
   // 32-bit buffer byte offsets
   TLOD_CHECK_ARG((size_t)std::max(M, N) * K * 4 < (1ull << 31), "operand too large");
+  if (gemm_ws_applies(M, N, K, nprod))
+    return gemm_ws_launch(a, b, bias, nullptr, 0, c, M, N, K, a_kcontig, b_kcontig, ws, ws_bytes,
+                          (hipStream_t)stream);
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
     return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   });
+}
+
+extern "C" int tlod_gemm_bs_ex_f32(const float* a, const float* b, const float* bias,
+                                   const float* residual, int relu, float* c, int M, int N, int K,
+                                   int a_kcontig, int b_kcontig, int nprod, void* ws,
+                                   size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(M > 0 && N > 0 && K > 0 && a && b && c, "bad arguments");
+  TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
+  TLOD_CHECK_ARG(residual != c || residual == nullptr, "residual must not alias c");
+  TLOD_CHECK_ARG((size_t)std::max(M, N) * K * 4 < (1ull << 31), "operand too large");
+  if (gemm_ws_applies(M, N, K, nprod))
+    return gemm_ws_launch(a, b, bias, residual, relu, c, M, N, K, a_kcontig, b_kcontig, ws,
+                          ws_bytes, (hipStream_t)stream);
+  const int st = with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
+    return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+  });
+  if (st != kOk || (residual == nullptr && !relu)) return st;
+  const size_t n = (size_t)M * N;
+  hipLaunchKernelGGL(gemm_res_act_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)),
+                     dim3(256), 0, (hipStream_t)stream, c, residual, relu, n);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
 }
 
 extern "C" size_t tlod_conv3x3_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
@@ -886,7 +954,8 @@ extern "C" int tlod_conv3x3_gemm_bs_f32(const float* x, const float* w, int w_la
   TLOD_CHECK_ARG(w_layout == 0 || w_layout == 1, "w_layout must be 0 or 1");
   TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
   // 32-bit buffer byte offsets
-  TLOD_CHECK_ARG((size_t)N * Cin * H * W * 4 < (1ull << 31) && (size_t)Cout * Cin * 9 * 4 < (1ull << 31),
+  TLOD_CHECK_ARG((size_t)N * Cin * H * W * 4 < (1ull << 31) && (size_t)Cout * Cin * 9 * 4 < (1ull << 31) &&
+                     (size_t)Cout * H * W * 4 < (1ull << 31),
                  "operand too large");
   return with_conv_gemm(w_layout, nprod, [&](auto g) {
     return g.run(x, w, ConvEpi{scale, bias, residual, relu}, y, N, Cin, H, W, Cout,
@@ -910,8 +979,9 @@ extern "C" int tlod_conv1x1_gemm_bs_f32(const float* x, const float* w, int w_la
   TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
   TLOD_CHECK_ARG(w_layout == 0 || w_layout == 1, "w_layout must be 0 or 1");
   TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
-  // 32-bit buffer byte offsets (per image for x)
-  TLOD_CHECK_ARG((size_t)Cin * H * W * 4 < (1ull << 31) && (size_t)Cout * Cin * 4 < (1ull << 31),
+  // 32-bit buffer byte offsets (per image for x and y)
+  TLOD_CHECK_ARG((size_t)Cin * H * W * 4 < (1ull << 31) && (size_t)Cout * Cin * 4 < (1ull << 31) &&
+                     (size_t)Cout * H * W * 4 < (1ull << 31),
                  "operand too large");
   return with_conv1x1_gemm(w_layout, nprod, N, H, W, Cout, [&](auto g) {
     return g.run(x, w, ConvEpi{scale, bias, residual, relu}, y, N, Cin, H, W, Cout,

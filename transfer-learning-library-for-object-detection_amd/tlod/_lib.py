@@ -106,6 +106,8 @@ SIGNATURES = {
     "tlod_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "tlod_gemm_bs_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                  c_size_t, P]),
+    "tlod_gemm_bs_ex_f32": (c_int, [P, P, P, P, c_int, P, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, P, c_size_t, P]),
     "tlod_conv3x3_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
                                                         c_int]),
     "tlod_conv3x3_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from .. import _lib
 from ..conv import ConvBNFunction
-from ..linear import LinearFunction, linear_math
+from ..linear import LinearActFunction, LinearFunction, linear_math
 
 
 def fold_bn(bn):
@@ -168,11 +168,14 @@ class Bottleneck(nn.Module):
         m = linear_math()
         if m == "f32":
             y = torch.addmm(shift, xm, (wm * scale[:, None]).t())
-        else:
-            y = LinearFunction.apply(xm.contiguous(), wm * scale[:, None], shift, m)
-        if residual is not None:
-            y = y.add_(residual)
-        return F.relu(y, inplace=True) if relu else y
+            if residual is not None:
+                y = y.add_(residual)
+            return F.relu(y, inplace=True) if relu else y
+        if residual is None and not relu:
+            return LinearFunction.apply(xm.contiguous(), wm * scale[:, None], shift, m)
+        # residual add and ReLU in the GEMM epilogue (tlod_gemm_bs_ex_f32)
+        return LinearActFunction.apply(xm.contiguous(), wm * scale[:, None], shift, residual,
+                                       relu, m)
 
     def forward_nhwc(self, x):
         """x: (R, H, W, C) channels-last (the layer4 RoI head)."""

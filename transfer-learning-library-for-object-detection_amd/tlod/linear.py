@@ -29,9 +29,11 @@ def linear_math():
     return m
 
 
-def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6", out=None):
-    """c[M][N] = sum_k A(m,k) B(n,k) (+ bias[n]) — see include/tlod.h tlod_gemm_bs_f32.
-    ``out``: a contiguous (M, N) float32 tensor to write into."""
+def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6", out=None,
+         residual=None, relu=False):
+    """c[M][N] = act(sum_k A(m,k) B(n,k) (+ bias[n]) (+ residual[m][n])) — see include/tlod.h
+    tlod_gemm_bs_f32 / tlod_gemm_bs_ex_f32.  ``out``: a contiguous (M, N) float32 tensor to
+    write into."""
     _lib.require_cuda(a, b)
     if a.dtype != torch.float32 or b.dtype != torch.float32:
         raise TypeError("tlod gemm computes in fp32 (the reference's dtype)")
@@ -44,10 +46,20 @@ def gemm(a, b, M, N, K, a_kcontig, b_kcontig, bias=None, math="bf16x6", out=None
                         a.device, "gemm")
     bias = bias.detach().contiguous() if bias is not None else None
     from .conv import _timed  # bench.py's launch timing (tlod.conv.PROFILE), shape (M, N, K)
+    if residual is None and not relu:
+        _timed("gemm", (M, N, K), lambda: _lib.check(
+            L.tlod_gemm_bs_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K,
+                               int(a_kcontig), int(b_kcontig), nprod, _lib.ptr(ws), ws.numel(),
+                               _lib.stream_of(a)), "gemm_bs"), math)
+        return c
+    if residual is not None:
+        residual = residual.detach().contiguous()
+        assert residual.shape == (M, N) and residual.dtype == torch.float32
     _timed("gemm", (M, N, K), lambda: _lib.check(
-        L.tlod_gemm_bs_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K,
-                           int(a_kcontig), int(b_kcontig), nprod, _lib.ptr(ws), ws.numel(),
-                           _lib.stream_of(a)), "gemm_bs"), math)
+        L.tlod_gemm_bs_ex_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(residual),
+                              int(relu), _lib.ptr(c), M, N, K, int(a_kcontig), int(b_kcontig),
+                              nprod, _lib.ptr(ws), ws.numel(), _lib.stream_of(a)), "gemm_bs_ex"),
+        math)
     return c
 
 
@@ -79,6 +91,43 @@ class LinearFunction(torch.autograd.Function):
             slot = grad_out(ctx.params[1])
             db = dy.sum(0) if slot is None else torch.sum(dy, 0, out=slot)
         return dx, dw, db, None
+
+
+class LinearActFunction(torch.autograd.Function):
+    """y = act(x W^T + bias + residual) in one GEMM launch (the ResNet RoI head's bottleneck
+    convs as GEMMs with the folded BN shift as the bias, lib/DAF/resnet.py Bottleneck:
+    out = relu(bn3(conv3(...)) + residual)).  Backward: g = dy * (y > 0), then the GEMMs of
+    LinearFunction; the residual's gradient is g."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, relu, math):
+        R, I = x.shape
+        O = weight.shape[0]
+        y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math, residual=residual, relu=relu)
+        ctx.math, ctx.relu = math, relu
+        ctx.has_bias, ctx.has_res = bias is not None, residual is not None
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        R, I = x.shape
+        O = weight.shape[0]
+        g = dy.contiguous()
+        if ctx.relu:
+            g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math)
+        if ctx.needs_input_grad[1]:
+            dw = gemm(g, x, O, I, R, 0, 0, None, ctx.math, out=grad_out(ctx.params[0]))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            slot = grad_out(ctx.params[1])
+            db = g.sum(0) if slot is None else torch.sum(g, 0, out=slot)
+        dres = g if ctx.has_res and ctx.needs_input_grad[3] else None
+        return dx, dw, db, dres, None, None
 
 
 class Linear(nn.Linear):
