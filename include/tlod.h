@@ -347,6 +347,14 @@ int tlod_conv1x1_gemm_bs_f32(const float* x, const float* w, int w_layout, const
                              const float* bias, const float* residual, float* y, int N, int Cin,
                              int H, int W, int Cout, int relu, int nprod, void* ws,
                              size_t ws_bytes, tlod_stream_t stream);
+/* tlod_conv1x1_gemm_bs_f32 with a final y *= (mask > 0) (mask (N, Cout, H, W), may be NULL,
+ * must not alias y): the dgrad form (w_layout = 1) of a ResNet bottleneck conv1 / conv3 with
+ * the previous layer's ReLU backward in the epilogue, after the residual (the identity
+ * shortcut's gradient) is added.  Same workspace. */
+int tlod_conv1x1_gemm_bs_ex_f32(const float* x, const float* w, int w_layout, const float* scale,
+                                const float* bias, const float* residual, const float* mask,
+                                float* y, int N, int Cin, int H, int W, int Cout, int relu,
+                                int nprod, void* ws, size_t ws_bytes, tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ Max pooling
  * Replaces: nn.MaxPool2d(kernel_size=2, stride=2) (floor mode) in RCNN_base (torchvision

@@ -236,6 +236,63 @@ def test_conv1x1_gemm_fwd_dgrad(math, N, Cin, Cout, H, W):
     _close(dx, torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double()), math)
 
 
+@pytest.mark.parametrize("N,Cin,Cout,H,W", ONE_SHAPES[:4] + ONE_SHAPES[5:6])
+def test_conv1x1_dgrad_residual_mask(N, Cin, Cout, H, W):
+    """The 1x1 dgrad epilogue with a residual gradient and the previous layer's ReLU mask
+    (tlod_conv1x1_gemm_bs_ex_f32): bit-identical to (dgrad + residual) * (mask > 0), including
+    split-K tail tiles, and tagged as masked."""
+    from tlod.conv import conv_dgrad
+    g = torch.Generator().manual_seed(5 + Cin + H)
+    gy = torch.randn(N, Cout, H, W, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 1, 1, generator=g) * (2.0 / Cin) ** 0.5).to(dev)
+    m = torch.relu(torch.randn(N, Cin, H, W, generator=g)).to(dev)
+    r = torch.randn(N, Cin, H, W, generator=g).to(dev)
+    a = conv_dgrad(gy, w, math="bf16x6", mask=m, residual=r)
+    b = (conv_dgrad(gy, w, math="bf16x6") + r) * (m > 0)
+    assert torch.equal(a, b)
+    assert a._tlod_relu_masked[0] == m.data_ptr()
+    c = conv_dgrad(gy, w, math="bf16x6", mask=m)
+    assert torch.equal(c, conv_dgrad(gy, w, math="bf16x6") * (m > 0))
+
+
+def test_bottleneck_shortcut_link_matches_unfused(monkeypatch):
+    """Two identity ResNet bottlenecks (layer3-like widths): with the ShortcutLink the
+    shortcut gradient is added in conv1's dgrad epilogue before the previous block's ReLU
+    mask, and the masked gradient skips that block's ReLU-backward pass; input and weight
+    gradients equal the unlinked backward's (the same kernels, summed in the same order)."""
+    import tlod.conv as tc
+    from tlod.detector import resnet as rn
+    torch.manual_seed(4)
+    blocks = torch.nn.Sequential(rn.Bottleneck(512, 128), rn.Bottleneck(512, 128)).to(dev)
+    for m in blocks.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.eval()
+            m.weight.requires_grad_(False)
+            m.bias.requires_grad_(False)
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+    x0 = torch.relu(torch.randn(2, 512, 19, 38)).to(dev)
+    gy = torch.randn(2, 512, 19, 38).to(dev)
+
+    def run():
+        blocks.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = tc.ConvBNFunction.apply(x, torch.ones(512, 512, 1, 1, device=dev) * 0.01,
+                                    torch.ones(512, device=dev), torch.zeros(512, device=dev),
+                                    None, True, None, 0)  # a ReLU output feeding block 0
+        blocks(y).backward(gy)
+        return [x.grad] + [p.grad.clone() for p in blocks.parameters() if p.requires_grad]
+    before = dict(tc.STATS)
+    linked = run()
+    n_skip = tc.STATS["relu_bwd_skipped"] - before["relu_bwd_skipped"]
+    monkeypatch.setattr(rn, "ShortcutLink", lambda: None)
+    before = dict(tc.STATS)
+    plain = run()
+    assert n_skip > tc.STATS["relu_bwd_skipped"] - before["relu_bwd_skipped"]
+    for a, b in zip(linked, plain):
+        _close(a, b.double(), "bf16x6")
+
+
 def test_conv_bs_matches_f32_path_closely():
     """bf16x6 and the f32-input MFMA path agree to f32 rounding on a conv3_3 shape."""
     from tlod.conv import conv_fwd

@@ -26,7 +26,11 @@ def timeit(fn, iters=20, warmup=3):
 
 out = {}
 R = 556
-for name, I, O in (("fc6", 25088, 4096), ("fc7", 4096, 4096)):
+LAYERS = [("fc6", 25088, 4096), ("fc7", 4096, 4096)]
+if "--r101" in sys.argv:  # the DAF-R101 RoI head's layer4 GEMMs: 428 RoIs x 16 bins (4 x 4)
+    R = 6848
+    LAYERS = [("l4_conv1", 2048, 512), ("l4_conv2", 4608, 512), ("l4_conv3", 512, 2048)]
+for name, I, O in LAYERS:
     x = torch.randn(R, I, device="cuda")
     w = torch.randn(O, I, device="cuda") * 0.01
     dy = torch.randn(R, O, device="cuda")

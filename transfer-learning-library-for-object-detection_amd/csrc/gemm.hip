@@ -559,6 +559,7 @@ struct ConvEpi {
   const float* bias;
   const float* residual;
   int relu;
+  const float* mask = nullptr;  // y *= (mask > 0) last: a dgrad's previous-layer ReLU backward
 };
 
 template <int NPL>
@@ -715,6 +716,8 @@ conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, C
   const i32x4 y_rsrc = make_buffer_rsrc(Y + ybase, (unsigned)Cout * (unsigned)P * 4u);
   const i32x4 r_rsrc = make_buffer_rsrc(epi.residual ? epi.residual + ybase : Y + ybase,
                                         epi.residual ? (unsigned)Cout * (unsigned)P * 4u : 0u);
+  const i32x4 k_rsrc = make_buffer_rsrc(epi.mask ? epi.mask + ybase : Y + ybase,
+                                        epi.mask ? (unsigned)Cout * (unsigned)P * 4u : 0u);
   int pix4[kAccCols];
 #pragma unroll
   for (int j = 0; j < kAccCols; ++j) {
@@ -723,14 +726,17 @@ conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, C
   }
 #pragma unroll
   for (int i = 0; i < acc_rows<MI>(); ++i) {
-    float res[kAccRegs][kAccCols];
-    if (epi.residual) {
+    float res[kAccRegs][kAccCols], msk[kAccRegs][kAccCols];
+    if (epi.residual || epi.mask) {
 #pragma unroll
       for (int r = 0; r < kAccRegs; ++r) {
         const int co = m0 + wm * MI * 32 + acc_row(i, r, lane);
 #pragma unroll
-        for (int j = 0; j < kAccCols; ++j)
-          res[r][j] = raw_buffer_load_f32(r_rsrc, co < Cout && pix4[j] != kBufOOB ? co * P * 4 + pix4[j] : kBufOOB, 0, 0);
+        for (int j = 0; j < kAccCols; ++j) {
+          const int o = co < Cout && pix4[j] != kBufOOB ? co * P * 4 + pix4[j] : kBufOOB;
+          res[r][j] = epi.residual ? raw_buffer_load_f32(r_rsrc, o, 0, 0) : 0.f;
+          msk[r][j] = epi.mask ? raw_buffer_load_f32(k_rsrc, o, 0, 0) : 1.f;
+        }
       }
     }
 #pragma unroll
@@ -745,6 +751,7 @@ conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, C
         v += bi;
         if (epi.residual) v += res[r][j];
         if (epi.relu) v = fmaxf(v, 0.f);
+        if (epi.mask) v = msk[r][j] > 0.f ? v : 0.f;
         raw_buffer_store_f32(v, y_rsrc, co < Cout && pix4[j] != kBufOOB ? co * P * 4 + pix4[j] : kBufOOB, 0, 0);
       }
     }
@@ -776,6 +783,7 @@ __global__ void __launch_bounds__(256) conv_tail_reduce_kernel(
     if (epi.bias) v += epi.bias[co];
     if (epi.residual) v += epi.residual[idx];
     if (epi.relu) v = fmaxf(v, 0.f);
+    if (epi.mask) v = epi.mask[idx] > 0.f ? v : 0.f;
     Y[idx] = v;
   }
 }
@@ -968,6 +976,28 @@ extern "C" size_t tlod_conv1x1_gemm_bs_workspace_bytes(int N, int Cin, int H, in
   if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0 || (nprod != 3 && nprod != 6)) return 0;
   return with_conv1x1_gemm(w_layout, nprod, N, H, W, Cout,
                            [&](auto g) { return g.ws_bytes(N, Cin, H, W, Cout); });
+}
+
+extern "C" int tlod_conv1x1_gemm_bs_ex_f32(const float* x, const float* w, int w_layout,
+                                           const float* scale, const float* bias,
+                                           const float* residual, const float* mask, float* y,
+                                           int N, int Cin, int H, int W, int Cout, int relu,
+                                           int nprod, void* ws, size_t ws_bytes,
+                                           tlod_stream_t stream) {
+  TLOD_CHECK_ARG(mask != y || mask == nullptr, "mask must not alias y");
+  ConvEpi e{scale, bias, residual, relu};
+  e.mask = mask;
+  TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0 && x && w && y, "bad arguments");
+  TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
+  TLOD_CHECK_ARG(w_layout == 0 || w_layout == 1, "w_layout must be 0 or 1");
+  TLOD_CHECK_ARG(residual != y || residual == nullptr, "residual must not alias y");
+  TLOD_CHECK_ARG((size_t)Cin * H * W * 4 < (1ull << 31) && (size_t)Cout * Cin * 4 < (1ull << 31) &&
+                     (size_t)Cout * H * W * 4 < (1ull << 31),
+                 "operand too large");
+  return with_conv1x1_gemm(w_layout, nprod, N, H, W, Cout, [&](auto g) {
+    return g.run(x, w, e, y, N, Cin, H, W, Cout, static_cast<float*>(ws), ws_bytes,
+                 (hipStream_t)stream);
+  });
 }
 
 extern "C" int tlod_conv1x1_gemm_bs_f32(const float* x, const float* w, int w_layout,

@@ -116,6 +116,8 @@ SIGNATURES = {
                                                         c_int]),
     "tlod_conv1x1_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, P, c_size_t, P]),
+    "tlod_conv1x1_gemm_bs_ex_f32": (c_int, [P, P, c_int, P, P, P, P, P, c_int, c_int, c_int,
+                                            c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "tlod_maxpool2x2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_maxpool2x2_relu_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),
     "tlod_conv_fwd_bs_pool_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -99,7 +99,7 @@ def _gemm1x1(KS, math, cin, cout):
             and os.environ.get("TLOD_CONV1X1_BS", "1") != "0")
 
 
-def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS=3):
+def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS=3, mask=None):
     N, Cin, H, W = x.shape
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
@@ -115,6 +115,16 @@ def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS
                       "conv1x1_gemm_bs"))
     ws = _lib.workspace(wsb(N, Cin, H, W, Cout, w_layout, nprod), x.device, "conv")
     shape = (N, Cin, H, W, Cout, KS) if kind == "fwd" else (N, Cout, H, W, Cin, KS)
+    if mask is not None:  # 1x1 only: y *= (mask > 0) last (tlod_conv1x1_gemm_bs_ex_f32)
+        assert KS == 1 and mask.shape == y.shape, (KS, mask.shape, y.shape)
+        mk = mask.detach().contiguous()
+        _timed(kind, shape, lambda: _lib.check(
+            L.tlod_conv1x1_gemm_bs_ex_f32(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc),
+                                          _lib.ptr(b), _lib.ptr(res), _lib.ptr(mk), _lib.ptr(y),
+                                          N, Cin, H, W, Cout, int(relu), nprod, _lib.ptr(ws),
+                                          ws.numel(), _lib.stream_of(x)), "conv1x1_gemm_bs_ex"),
+            math)
+        return y
     _timed(kind, shape, lambda: _lib.check(
         fn(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc), _lib.ptr(b), _lib.ptr(res),
            _lib.ptr(y), N, Cin, H, W, Cout, int(relu), nprod, _lib.ptr(ws), ws.numel(),
@@ -242,15 +252,27 @@ def _conv_bs(x, wp, bias, relu, scale, residual, Cout, KS, math, kind):
     return y
 
 
-def conv_dgrad(g, weight, wd=None, math=None, mask=None):
+def conv_dgrad(g, weight, wd=None, math=None, mask=None, residual=None):
     """Input gradient.  mask (the conv's input, when that is the previous conv's ReLU output):
-    on the split-bf16 3x3 path the result is dx * (mask > 0) — the previous layer's ReLU
-    backward done in this epilogue (tlod_conv_dgrad_bs_mask_f32) — and it is tagged so that
-    layer's backward skips its own pass (ConvFunction); other paths ignore mask."""
+    on the split-bf16 3x3 path and the split-bf16 1x1 GEMM the result is dx * (mask > 0) — the
+    previous layer's ReLU backward done in this epilogue (tlod_conv_dgrad_bs_mask_f32,
+    tlod_conv1x1_gemm_bs_ex_f32) — and it is tagged so that layer's backward skips its own pass
+    (ConvFunction, ConvBNFunction); other paths ignore mask.  residual (1x1 GEMM path, or
+    added here otherwise): a gradient summed into dx before the mask (a bottleneck's identity
+    shortcut)."""
     g = g.contiguous()
     N, Cout, H, W = g.shape
     _, Cin, KS, _ = weight.shape
     math = conv_math() if math is None else math
+    if _gemm1x1(KS, math, Cout, Cin) and (mask is not None or residual is not None):
+        dx = _conv_gemm(g, weight.detach().contiguous(), 1, None, False, None, residual, Cin,
+                        math, "dgrad", KS=1, mask=mask)
+        if mask is not None:
+            dx._tlod_relu_masked = (mask.data_ptr(), dx.data_ptr(), dx._version)
+            STATS["masked_dgrad"] += 1
+        return dx
+    if residual is not None:
+        return conv_dgrad(g, weight, wd, math).add_(residual)
     if mask is not None and _bs(KS, math) and not _gemm_conv(KS, math, Cin):
         return _conv_dgrad_mask(g, pack_bs(weight, True) if wd is None else wd, mask, Cin, math)
     if _gemm_conv(KS, math, Cin):
@@ -419,17 +441,32 @@ def relu_bwd_ex(dy, y=None, scale=None, want_raw=False):
     return g, raw
 
 
+class ShortcutLink:
+    """Hands an identity bottleneck's shortcut gradient from its conv3's backward (which runs
+    first) to its conv1's backward, whose input is the same tensor: conv1's dgrad adds it in
+    the epilogue before the previous block's ReLU mask (tlod_conv1x1_gemm_bs_ex_f32), instead
+    of autograd summing the two gradients and the previous block running a ReLU-backward pass
+    over the sum."""
+
+    def __init__(self):
+        self.g = None
+
+
 class ConvBNFunction(torch.autograd.Function):
     """Bias-free conv + frozen BatchNorm (per-channel scale/shift) (+ residual) (+ ReLU), the
-    ResNet bottleneck's conv->bn(->add)->relu (lib/DAF/resnet.py:80-99) in one kernel."""
+    ResNet bottleneck's conv->bn(->add)->relu (lib/DAF/resnet.py:80-99) in one kernel.
+    link (a ShortcutLink) with role 3: this conv's residual is its block's input and its
+    gradient goes to the link; role 1: this conv reads the block's input and adds the link's
+    gradient to its own input gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, scale, shift, residual, relu):
+    def forward(ctx, x, weight, scale, shift, residual, relu, link=None, role=0):
         y = conv_fwd(x, weight, shift, relu, scale=scale, residual=residual)
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.wparam = weight
         ctx.mask_in = _relu_out(x)
+        ctx.link, ctx.role = link, role
         ctx.save_for_backward(x, weight, scale, y if relu else None)
         if relu:
             y._tlod_relu_out = True
@@ -437,10 +474,20 @@ class ConvBNFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        dx, dw, g_res = ConvBNFunction._backward(ctx, dy)
+        if ctx.role == 3 and ctx.link is not None and g_res is not None:
+            ctx.link.g, g_res = g_res, None  # to conv1's backward (ShortcutLink)
+        return (dx, dw, None, None, g_res, None, None, None)[:len(ctx.needs_input_grad)]
+
+    @staticmethod
+    def _backward(ctx, dy):
         x, weight, scale, y = ctx.saved_tensors
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         mask = x if ctx.mask_in else None
+        res = None
+        if ctx.role == 1 and ctx.link is not None:
+            res, ctx.link.g = ctx.link.g, None
         if (ctx.relu and y is not None and
                 getattr(dy, "_tlod_relu_masked", None) == (y.data_ptr(), dy.data_ptr(), dy._version)):
             # dy is the next conv's dgrad, already masked by this ReLU (a bottleneck's 3x3 conv2
@@ -448,16 +495,16 @@ class ConvBNFunction(torch.autograd.Function):
             # (W * scale per output channel) and the weight gradient's rows — no pass over dy
             STATS["relu_bwd_skipped"] += 1
             s4 = scale.detach().view(-1, 1, 1, 1)
-            dx = conv_dgrad(dy, weight.detach() * s4, mask=mask) if need_x else None
+            dx = conv_dgrad(dy, weight.detach() * s4, mask=mask, residual=res) if need_x else None
             dw = None
             if need_w:
                 dw = conv_wgrad(dy, x, weight.shape[2], out=grad_out(ctx.wparam))
                 dw.mul_(s4)
-            return dx, dw, None, None, dy if need_res else None, None
+            return dx, dw, dy if need_res else None
         g, g_raw = relu_bwd_ex(dy, y if ctx.relu else None, scale, want_raw=need_res)
-        dx = conv_dgrad(g, weight, mask=mask) if need_x else None
+        dx = conv_dgrad(g, weight, mask=mask, residual=res) if need_x else None
         dw = conv_wgrad(g, x, weight.shape[2], out=grad_out(ctx.wparam)) if need_w else None
-        return dx, dw, None, None, g_raw, None
+        return dx, dw, g_raw
 
 
 def maxpool2x2(x):

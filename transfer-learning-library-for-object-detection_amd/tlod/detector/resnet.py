@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
-from ..conv import ConvBNFunction
+from ..conv import ConvBNFunction, ShortcutLink
 from ..linear import LinearActFunction, LinearFunction, linear_math
 
 
@@ -105,9 +105,9 @@ def im2col3x3_nhwc(x):
                      3).reshape(R * H * W, 9 * P)
 
 
-def conv_bn(x, conv, bn, relu, residual=None):
+def conv_bn(x, conv, bn, relu, residual=None, link=None, role=0):
     scale, shift = fold_bn(bn)
-    return ConvBNFunction.apply(x, conv.weight, scale, shift, residual, relu)
+    return ConvBNFunction.apply(x, conv.weight, scale, shift, residual, relu, link, role)
 
 
 def stem(x, conv1, bn1):
@@ -149,11 +149,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         xs = Subsample2Function.apply(x) if self.stride == 2 else x
-        out = self._tap("r1", conv_bn(xs, self.conv1, self.bn1, relu=True))
+        # identity shortcut: conv1's dgrad takes the shortcut's gradient (ShortcutLink)
+        link = ShortcutLink() if self.downsample is None and self.stride == 1 else None
+        out = self._tap("r1", conv_bn(xs, self.conv1, self.bn1, relu=True, link=link, role=1))
         out = self._tap("r2", conv_bn(out, self.conv2, self.bn2, relu=True))
         res = (conv_bn(xs, self.downsample[0], self.downsample[1], relu=False)
                if self.downsample is not None else x)
-        return self._tap("r3", conv_bn(out, self.conv3, self.bn3, relu=True, residual=res))
+        return self._tap("r3", conv_bn(out, self.conv3, self.bn3, relu=True, residual=res,
+                                       link=link, role=3))
 
     # ---------------------------------------------------------------- RoI head path
     @staticmethod
