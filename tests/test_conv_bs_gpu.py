@@ -439,3 +439,4 @@ def test_pack_bs_bit_exact(Cout, Cin, dgrad):
     ref = _ref_pack(w, dgrad)
     assert p.numel() == ref.numel()
     assert torch.equal(p, ref)
+

@@ -47,11 +47,6 @@ __device__ __forceinline__ float bf_hi(unsigned p) { return __uint_as_float(p & 
 // per packed op in an MFMA stream), and a producer wave sharing its SIMD with MFMA waves
 // issued them at a fraction of the plain rate (wgrad_ws producers: ~48 cycles per
 // instruction with the compiler's packed split).
-__device__ __forceinline__ float add_f32(float a, float b) {  // unpacked, as sub_f32
-  float r;
-  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 __device__ __forceinline__ float sub_f32(float a, float b) {
   float r;
   asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));

@@ -869,10 +869,7 @@ __device__ __forceinline__ void bs_mac16(f32x4& acc, const V (&a)[3], const V (&
       t = mf(a[1], b[1], t);
       t = mf(a[0], b[2], t);
     }
-    t = mf(a[0], b[0], t);
-    // single-lane adds: a v_pk_add_f32 between MFMAs serialises with the matrix pipe
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc[e] = add_f32(acc[e], t[e]);
+    acc += mf(a[0], b[0], t);
     return;
   }
   acc = mf(a[0], b[0], acc);

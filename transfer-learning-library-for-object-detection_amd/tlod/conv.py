@@ -133,16 +133,27 @@ def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS
     return y
 
 
+# Writes to frozen weights that bypass torch's version counter (the data-parallel start-up
+# broadcast, tlod.dist, writes through .data) bump this, so the cached packs are remade.
+_EXTERNAL_WRITES = [0]
+
+
+def weights_updated():
+    """Called after a write to parameters that did not bump their version counters."""
+    _EXTERNAL_WRITES[0] += 1
+
+
 def pack_bs(weight, dgrad):
     """Pre-split bf16 planes of a 3x3 weight for the split-bf16 fwd (dgrad=0) / dgrad (1).
     Frozen weights (requires_grad False: conv1/conv2 of VGG16, the fixed ResNet blocks) are
     packed once per (storage, version), cached on the tensor itself — an in-place load bumps
-    the version; trainable weights are repacked every call (the fused SGD writes them
-    without a version bump).  One cached pack per tensor (a frozen weight is packed for the
-    forward only)."""
+    the version, a write that bypasses it (the data-parallel broadcast) calls
+    weights_updated().  Trainable weights are repacked every call (the fused SGD
+    writes them without a version bump; packing all of them in one launch per step,
+    tried in round 4, was no faster).  One cached pack per tensor."""
     if not weight.requires_grad:
         cache = getattr(weight, "_tlod_packs", None)  # lives and dies with the tensor
-        key = (weight.data_ptr(), weight._version, bool(dgrad))
+        key = (weight.data_ptr(), weight._version, bool(dgrad), _EXTERNAL_WRITES[0])
         if cache is None or cache[0] != key:
             cache = (key, _pack_bs(weight, dgrad))
             weight._tlod_packs = cache

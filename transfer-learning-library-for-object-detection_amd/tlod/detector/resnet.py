@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
+from .. import conv as conv_mod
 from ..conv import ConvBNFunction, ShortcutLink
 from ..linear import LinearActFunction, LinearFunction, linear_math
 
@@ -31,13 +32,14 @@ from ..linear import LinearActFunction, LinearFunction, linear_math
 def fold_bn(bn):
     """Frozen eval-mode BatchNorm as y = x * scale + shift (per channel).  Cached on the
     module and recomputed only when one of its four tensors changes: a different tensor object
-    (reassignment, load_state_dict(assign=True)) or an in-place write (its version counter).
+    (reassignment, load_state_dict(assign=True)), an in-place write (its version counter) or
+    a write that bypasses it (tlod.conv.weights_updated: the data-parallel broadcast).
     The cache holds the four tensors themselves, so a replaced tensor's storage cannot be
     reused at the same address while its fold is cached.  ResNet101 has 104 BatchNorms, i.e.
     400+ small launches per forward otherwise."""
     assert not bn.weight.requires_grad, "tlod ResNet expects frozen BatchNorm (resnet.py:261-267)"
     ts = (bn.weight, bn.bias, bn.running_mean, bn.running_var)
-    vs = tuple(t._version for t in ts) + (bn.eps,)
+    vs = tuple(t._version for t in ts) + (bn.eps, conv_mod._EXTERNAL_WRITES[0])
     c = getattr(bn, "_tlod_fold", None)
     if c is not None and c[1] == vs and all(a is b for a, b in zip(c[0], ts)):
         return c[2], c[3]

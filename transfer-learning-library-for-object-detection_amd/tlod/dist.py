@@ -28,6 +28,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from .conv import weights_updated
 from .grads import GradArena, arena_of
 
 
@@ -60,6 +61,7 @@ class GradBucketReducer:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, dist.get_global_rank(group, 0) if group else 0,
                                group=group)
+        weights_updated()  # written through .data: no version bump
         if arena is None:
             arena = arena_of(params[0]) if params else None
             if arena is None or set(arena.params) != set(params):
