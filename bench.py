@@ -278,8 +278,9 @@ def main():
                                   "gflop_per_step": round(conv_f / a.steps / 1e9, 2)},
                      "by_kind": detail},
         "conv_math": {"3x3 fwd/dgrad": tconv.conv_math(), "3x3 and 1x1 wgrad": tconv.wgrad_math(),
-                      "1x1 fwd/dgrad": f"{tconv.conv_math()} (>= 64 channels; f32 MFMA for "
-                                       "the RPN cls/bbox heads)",
+                      "1x1 fwd/dgrad": f"{tconv.conv_math()} (>= 64 channels on one side, "
+                                       ">= 16 on the other; f32 MFMA for the 2-output DA "
+                                       "image head)",
                       "fc6/fc7/DA fc": linear_math()},
         "rank_ms_per_step": {"min": round(min(per_rank) / a.steps * 1e3, 3),
                              "max": round(max(per_rank) / a.steps * 1e3, 3),

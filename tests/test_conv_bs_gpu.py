@@ -209,15 +209,18 @@ ONE_SHAPES = [  # N, Cin, Cout, H, W: ResNet101 bottleneck 1x1s (layer2 / layer3
     # the 64-, 128- and 256-row tiles, ragged channel / pixel counts
     (2, 1024, 256, 38, 75), (2, 256, 1024, 38, 75), (2, 512, 128, 75, 150), (1, 64, 64, 30, 41),
     (3, 96, 80, 9, 33), (1, 72, 257, 5, 7), (2, 130, 200, 1, 3),
+    # the RPN cls / bbox heads on the base feature (18 / 36 outputs: mostly-padding M tiles)
+    (2, 512, 18, 37, 75), (2, 512, 36, 37, 75),
 ]
 
 
 @pytest.mark.parametrize("math", ["bf16x6", "bf16x3"])
 @pytest.mark.parametrize("N,Cin,Cout,H,W", ONE_SHAPES)
-def test_conv1x1_gemm_fwd_dgrad(math, N, Cin, Cout, H, W):
+def test_conv1x1_gemm_fwd_dgrad(math, N, Cin, Cout, H, W, monkeypatch):
     """1x1 forward (folded-BN scale / shift + residual + ReLU epilogue) and input gradient on
     the split-bf16 conv GEMM (tlod_conv1x1_gemm_bs_f32) vs fp64."""
     from tlod.conv import _gemm1x1, conv_dgrad, conv_fwd
+    monkeypatch.setenv("TLOD_CONV1X1_MIN", "16")  # the RPN heads' 18 / 36 outputs
     assert _gemm1x1(1, math, Cin, Cout)
     g = torch.Generator().manual_seed(N * 7 + Cin + Cout + H)
     x = torch.randn(N, Cin, H, W, generator=g)

@@ -90,12 +90,15 @@ def _gemm_conv(KS, math, out_channels):
 
 
 def _gemm1x1(KS, math, cin, cout):
-    """1x1 convs under a split-bf16 math with >= 64 input and output channels run their
-    forward / input gradient as per-image GEMMs on the split-bf16 conv GEMM
+    """1x1 convs under a split-bf16 math with >= 64 channels on one side and >= 16 on the
+    other run their forward / input gradient as per-image GEMMs on the split-bf16 conv GEMM
     (tlod_conv1x1_gemm_bs_f32: W (Cout x Cin) times the image's (Cin x HW) map, 64/128/256-row
-    tiles by Cout, the folded-BN / residual / ReLU epilogue); TLOD_CONV1X1_BS=0 keeps them on
-    the f32-input MFMA kernel."""
-    return (KS == 1 and math != "f32" and min(cin, cout) >= 64
+    tiles by Cout, the folded-BN / residual / ReLU epilogue) — the ResNet bottlenecks, the DA
+    image heads and (round 4) the RPN cls / bbox heads (18 / 36 outputs: a 64-row tile
+    mostly padding still beats the f32-input MFMA kernel's 6.6 TF); TLOD_CONV1X1_BS=0 keeps
+    them on the f32-input MFMA kernel."""
+    return (KS == 1 and math != "f32" and max(cin, cout) >= 64
+            and min(cin, cout) >= int(os.environ.get("TLOD_CONV1X1_MIN", "64"))
             and os.environ.get("TLOD_CONV1X1_BS", "1") != "0")
 
 
