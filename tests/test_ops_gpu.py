@@ -138,44 +138,6 @@ def test_roi_align_avg_bwd_gather(B, C, H, W, R, P, monkeypatch):
     np.testing.assert_allclose(a, ref, rtol=1e-5, atol=atol)
 
 
-_CSORT_SCRIPT = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from tlod.roi_align import RoIAlignAvg
-rng = np.random.default_rng(7)
-B, C, H, W, R = 2, 64, 37, 75, 556
-f = rng.standard_normal((B, C, H, W)).astype(np.float32)
-x1 = rng.uniform(0, W * 16 - 40, R); y1 = rng.uniform(0, H * 16 - 40, R)
-r = np.stack([rng.integers(0, B, R), x1, y1, x1 + rng.uniform(8, 600, R),
-              y1 + rng.uniform(8, 400, R)], 1).astype(np.float32)
-r = np.concatenate([r, np.tile(np.array([[0, 100., 90., 130., 121.]], np.float32), (300, 1))])
-ft = torch.from_numpy(f).cuda().requires_grad_(True)
-out = RoIAlignAvg(7, 7, 1.0 / 16)(ft, torch.from_numpy(r).cuda())
-out.backward(torch.from_numpy(rng.standard_normal(out.shape).astype(np.float32)).cuda())
-np.save(sys.argv[2], ft.grad.cpu().numpy())
-"""
-
-
-def test_roi_align_avg_bwd_counting_sort_matches_radix_sort(tmp_path):
-    """The gather's stable counting sort of the taps (tlod_roi_align_avg_bwd_f32, round 4)
-    puts them in the same order as hipCUB's stable radix sort (TLOD_ROI_CSORT=0, read once
-    per process: two child processes), so the gradients are bit-identical — including cells
-    under the 300 copies of one RoI (runs of thousands of taps)."""
-    import os
-    import subprocess
-    import sys
-    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                       "transfer-learning-library-for-object-detection_amd")
-    out = {}
-    for v in ("0", "1"):
-        path = str(tmp_path / f"g{v}.npy")
-        env = dict(os.environ, TLOD_ROI_CSORT=v, TLOD_ROI_BWD_GATHER="1")
-        subprocess.run([sys.executable, "-c", _CSORT_SCRIPT, pkg, path], env=env, check=True,
-                       timeout=240)
-        out[v] = np.load(path)
-    np.testing.assert_array_equal(out["0"], out["1"])
-
-
 @pytest.mark.parametrize("B,C,H,W,R", [(1, 64, 37, 62, 128), (2, 16, 20, 25, 40)])
 def test_roi_pool_fwd_bwd(B, C, H, W, R):
     from tlod.roi_pool import roi_pool_with_argmax

@@ -396,130 +396,6 @@ __global__ void __launch_bounds__(256) rbg_sample_grad_kernel(const float* __res
   }
 }
 
-// ---- stable counting sort of the taps by cell (round 4; replaces hipCUB's radix sort, ~8
-// launches, and the binary-search start pass).  The taps are cut into blocks of kCsT in
-// index order, one wave each; a block's per-cell counts come from the wave's ballot over
-// equal keys (no atomics), every cell's per-block offsets from an in-order scan over the
-// blocks, the cell starts from one scan over the cells; the scatter then places each tap at
-// start[cell] + (taps of that cell in earlier blocks) + (earlier taps of the cell in its own
-// block): the same order as the stable radix sort, so the gather sums bit-identically.
-constexpr int kCsT = 1024;
-
-// calls f(leader_key, group_mask) once per distinct key among the active lanes, in lane order
-// of the groups' first lanes; wave-uniform
-template <typename F>
-__device__ __forceinline__ void rbg_key_groups(unsigned key, bool active, F f) {
-  unsigned long long left = __ballot(active);
-  while (left) {
-    const int leader = __builtin_ctzll(left);
-    const unsigned lk = __builtin_amdgcn_readlane(key, leader);
-    const unsigned long long m = __ballot(active && key == lk);
-    f(lk, m);
-    left &= ~m;
-  }
-}
-
-// hist[b][c] = taps of cell c (c = 0..ncell, ncell: outside the map) in block b
-__global__ void __launch_bounds__(64) rbg_hist_kernel(const unsigned* __restrict__ keys, int n,
-                                                      int ncell1, int* __restrict__ hist) {
-  extern __shared__ int cnt[];
-  const int lane = threadIdx.x, b = blockIdx.x;
-  for (int c = lane; c < ncell1; c += 64) cnt[c] = 0;
-  __syncthreads();
-  const int i1 = min(n, (b + 1) * kCsT);
-  for (int i0 = b * kCsT; i0 < i1; i0 += 64) {
-    const bool act = i0 + lane < i1;
-    const unsigned k = act ? keys[i0 + lane] : 0u;
-    rbg_key_groups(k, act, [&](unsigned lk, unsigned long long m) {
-      if (lane == 0) cnt[lk] += __popcll(m);
-    });
-  }
-  __syncthreads();
-  for (int c = lane; c < ncell1; c += 64) hist[(size_t)b * ncell1 + c] = cnt[c];
-}
-
-// per cell: hist[b][c] -> taps of c in blocks < b (in place); total[c] = all of them
-__global__ void __launch_bounds__(256) rbg_colscan_kernel(int* __restrict__ hist, int nb,
-                                                          int ncell1, int* __restrict__ total) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= ncell1) return;
-  int s = 0, b = 0;
-  for (; b + 8 <= nb; b += 8) {  // 8 loads in flight
-    int v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = hist[(size_t)(b + u) * ncell1 + c];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      hist[(size_t)(b + u) * ncell1 + c] = s;
-      s += v[u];
-    }
-  }
-  for (; b < nb; ++b) {
-    const int v = hist[(size_t)b * ncell1 + c];
-    hist[(size_t)b * ncell1 + c] = s;
-    s += v;
-  }
-  total[c] = s;
-}
-
-// start[c] = sum of total[0..c) for c = 0..ncell (start[ncell] = the valid tap count); one
-// workgroup of 1024 threads, each scanning a run of consecutive cells
-__global__ void __launch_bounds__(1024) rbg_cellscan_kernel(const int* __restrict__ total,
-                                                            int ncell1, int* __restrict__ start) {
-  __shared__ int wsum[16];
-  const int t = threadIdx.x, per = (ncell1 + 1023) / 1024;
-  const int c0 = t * per, c1 = min(ncell1, c0 + per);
-  int local = 0;
-  for (int c = c0; c < c1; ++c) local += total[c];
-  // exclusive scan of the threads' sums: within the wave, then over the 16 waves
-  int incl = local;
-  const int lane = t & 63, w = t >> 6;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int base = 0;
-  for (int k = 0; k < w; ++k) base += wsum[k];
-  int run = base + incl - local;
-  for (int c = c0; c < c1; ++c) {
-    start[c] = run;
-    run += total[c];
-  }
-}
-
-// keys_s / vals_s[start[k] + hist[b][k] + rank of the tap among block b's earlier taps of k]
-__global__ void __launch_bounds__(64) rbg_scatter_kernel(const unsigned* __restrict__ keys,
-                                                         const unsigned* __restrict__ vals, int n,
-                                                         int ncell1, const int* __restrict__ start,
-                                                         const int* __restrict__ hist,
-                                                         unsigned* __restrict__ keys_s,
-                                                         unsigned* __restrict__ vals_s) {
-  extern __shared__ int cnt[];
-  const int lane = threadIdx.x, b = blockIdx.x;
-  for (int c = lane; c < ncell1; c += 64) cnt[c] = 0;
-  __syncthreads();
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  const int i1 = min(n, (b + 1) * kCsT);
-  for (int i0 = b * kCsT; i0 < i1; i0 += 64) {
-    const bool act = i0 + lane < i1;
-    const unsigned k = act ? keys[i0 + lane] : 0u;
-    const unsigned v = act ? vals[i0 + lane] : 0u;
-    rbg_key_groups(k, act, [&](unsigned lk, unsigned long long m) {
-      const int before = cnt[lk];  // every lane reads before lane 0 adds this chunk's group
-      if ((m >> lane) & 1ull) {
-        const int pos = start[lk] + hist[(size_t)b * ncell1 + lk] + before + __popcll(m & lt);
-        if ((unsigned)pos < (unsigned)n) {  // always, by construction (a guard, not a branch)
-          keys_s[pos] = k;
-          vals_s[pos] = v;
-        }
-      }
-      if (lane == 0) cnt[lk] = before + __popcll(m);
-    });
-  }
-}
-
 // one tap's contribution, roi_align_kernel.cu:137-140 (as align_scatter)
 __device__ __forceinline__ float tap_value(float g, float hr, float wr, int k) {
   const float om = 1.f - wr;
@@ -643,18 +519,7 @@ struct RbgWs {
   float *sg, *acc, *carry_head, *carry_tail;
   void* cub_tmp;
   size_t cub_bytes;
-  int *hist, *total;  // counting sort (rbg_csort_ok)
 };
-
-// The counting sort's per-cell counters live in LDS (one wave per block); larger maps keep
-// hipCUB's radix sort.  TLOD_ROI_CSORT=0 forces hipCUB (A/B; the order is the same).
-static bool rbg_csort_ok(size_t ncell) {
-  static const bool on = [] {
-    const char* v = getenv("TLOD_ROI_CSORT");
-    return v && *v == '1';  // opt-in until validated on the GPU
-  }();
-  return on && (ncell + 1) * sizeof(int) <= 48 * 1024;
-}
 
 static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, int ph, int pw) {
   const size_t S = (size_t)(ph + 1) * (pw + 1), n = (size_t)R * S * 4;
@@ -670,17 +535,10 @@ static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, 
   w.carry_head = cv.take<float>(nseg * C);
   w.carry_tail = cv.take<float>(nseg * C);
   w.flags = cv.take<int>(nseg);
-  const size_t ncell = (size_t)B * H * W;
   w.cub_bytes = 0;
-  w.hist = w.total = nullptr;
-  if (rbg_csort_ok(ncell)) {
-    w.hist = cv.take<int>(div_up((int)n, kCsT) * (ncell + 1));
-    w.total = cv.take<int>(ncell + 1);
-  } else {
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, w.cub_bytes, (const unsigned*)nullptr,
-                                             (unsigned*)nullptr, (const unsigned*)nullptr,
-                                             (unsigned*)nullptr, (int)n);
-  }
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, w.cub_bytes, (const unsigned*)nullptr,
+                                           (unsigned*)nullptr, (const unsigned*)nullptr,
+                                           (unsigned*)nullptr, (int)n);
   w.cub_tmp = cv.take<char>(w.cub_bytes);
   return align_up(cv.off, 256);
 }
@@ -849,27 +707,12 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale,
                        H, W, ph, pw, ncell, w.keys, w.vals, w.geo);
     TLOD_LAUNCH_CHECK();
-    if (w.hist != nullptr) {  // stable counting sort (see rbg_hist_kernel)
-      const int nb = div_up(n, kCsT), nc1 = (int)ncell + 1;
-      const size_t lds = (size_t)nc1 * sizeof(int);
-      hipLaunchKernelGGL(rbg_hist_kernel, dim3(nb), dim3(64), lds, s, w.keys, n, nc1, w.hist);
-      TLOD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(rbg_colscan_kernel, dim3(div_up(nc1, 256)), dim3(256), 0, s, w.hist, nb,
-                         nc1, w.total);
-      TLOD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(rbg_cellscan_kernel, dim3(1), dim3(1024), 0, s, w.total, nc1, w.start);
-      TLOD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(rbg_scatter_kernel, dim3(nb), dim3(64), lds, s, w.keys, w.vals, n, nc1,
-                         w.start, w.hist, w.keys_s, w.vals_s);
-      TLOD_LAUNCH_CHECK();
-    } else {
-      size_t cb = w.cub_bytes;
-      TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals,
-                                                  w.vals_s, n, 0, rbg_bits(ncell), s));
-      hipLaunchKernelGGL(rbg_start_kernel, dim3(div_up((int)ncell + 1, 256)), dim3(256), 0, s,
-                         w.keys_s, n, ncell, w.start);
-      TLOD_LAUNCH_CHECK();
-    }
+    size_t cb = w.cub_bytes;
+    TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s,
+                                                n, 0, rbg_bits(ncell), s));
+    hipLaunchKernelGGL(rbg_start_kernel, dim3(div_up((int)ncell + 1, 256)), dim3(256), 0, s,
+                       w.keys_s, n, ncell, w.start);
+    TLOD_LAUNCH_CHECK();
     hipLaunchKernelGGL(rbg_sample_grad_kernel, dim3(R, div_up(C, 64)), dim3(256), 0, s, top_grad,
                        C, ph, pw, w.sg);
     TLOD_LAUNCH_CHECK();

@@ -98,7 +98,7 @@ def _gemm1x1(KS, math, cin, cout):
     mostly padding still beats the f32-input MFMA kernel's 6.6 TF); TLOD_CONV1X1_BS=0 keeps
     them on the f32-input MFMA kernel."""
     return (KS == 1 and math != "f32" and max(cin, cout) >= 64
-            and min(cin, cout) >= int(os.environ.get("TLOD_CONV1X1_MIN", "64"))
+            and min(cin, cout) >= int(os.environ.get("TLOD_CONV1X1_MIN", "16"))
             and os.environ.get("TLOD_CONV1X1_BS", "1") != "0")
 
 
