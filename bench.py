@@ -195,7 +195,8 @@ def main():
     torch.cuda.synchronize()
 
     records = []
-    tconv.PROFILE = records
+    # TLOD_BENCH_NOPROF=1 (diagnostic): no per-launch events in the timed region (no roofline)
+    tconv.PROFILE = None if os.environ.get("TLOD_BENCH_NOPROF") == "1" else records
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

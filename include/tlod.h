@@ -268,6 +268,10 @@ int tlod_relu_bwd_ex_f32(const float* dy, const float* y, const float* scale, fl
 size_t tlod_conv_pack_bs_bytes(int Cout, int Cin, int KS, int dgrad);
 int tlod_conv_pack_bs(const float* weight, int Cout, int Cin, int KS, int dgrad, void* packed,
                       tlod_stream_t stream);
+/* tlod_conv_pack_bs of weight[co] * scale[co] (scale: Cout floats, a frozen BatchNorm's scale
+ * after the conv; NULL: 1), the product rounded to f32 before the split. */
+int tlod_conv_pack_bs_ex(const float* weight, const float* scale, int Cout, int Cin, int KS,
+                         int dgrad, void* packed, tlod_stream_t stream);
 size_t tlod_conv_fwd_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout, int KS,
                                         int nprod);
 int tlod_conv_fwd_bs_f32(const float* x, const void* wp, const float* scale, const float* bias,
@@ -285,6 +289,14 @@ size_t tlod_conv_wgrad_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout
 int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw, float* db, int accumulate,
                            int N, int Cin, int H, int W, int Cout, int KS, int nprod, void* ws,
                            size_t ws_bytes, tlod_stream_t stream);
+/* tlod_conv_wgrad_bs_f32 with dW[co] = (accumulate ? dW[co] : 0) + row_scale[co] * (the
+ * gradient) (row_scale: Cout floats, may be NULL): a frozen BatchNorm's scale after the conv
+ * (ResNet bottlenecks, lib/DAF/resnet.py:80-99) folded into the weight gradient's reduce
+ * instead of a pass over dW. */
+int tlod_conv_wgrad_bs_ex_f32(const float* dy, const float* x, float* dw, float* db,
+                              int accumulate, const float* row_scale, int N, int Cin, int H,
+                              int W, int Cout, int KS, int nprod, void* ws, size_t ws_bytes,
+                              tlod_stream_t stream);
 /* Direct 3x3 conv (stride 1, pad 1) for Cin <= 4 — VGG16 conv1_1 on the image
  * (lib/DAF/vgg16.py:49 features[0]): y = act(conv(x, weight) + bias), weight the nn.Conv2d
  * (Cout, Cin, 3, 3) tensor as is, exact f32 FMA chains (27 per output for Cin = 3). */
@@ -350,11 +362,14 @@ int tlod_conv1x1_gemm_bs_f32(const float* x, const float* w, int w_layout, const
 /* tlod_conv1x1_gemm_bs_f32 with a final y *= (mask > 0) (mask (N, Cout, H, W), may be NULL,
  * must not alias y): the dgrad form (w_layout = 1) of a ResNet bottleneck conv1 / conv3 with
  * the previous layer's ReLU backward in the epilogue, after the residual (the identity
- * shortcut's gradient) is added.  Same workspace. */
+ * shortcut's gradient) is added.  w_scale (w_layout = 1 only, may be NULL): the weight taken as
+ * W[co][ci] * w_scale[co] (a frozen BatchNorm's scale after the conv), applied as it is
+ * staged.  Same workspace. */
 int tlod_conv1x1_gemm_bs_ex_f32(const float* x, const float* w, int w_layout, const float* scale,
                                 const float* bias, const float* residual, const float* mask,
-                                float* y, int N, int Cin, int H, int W, int Cout, int relu,
-                                int nprod, void* ws, size_t ws_bytes, tlod_stream_t stream);
+                                const float* w_scale, float* y, int N, int Cin, int H, int W,
+                                int Cout, int relu, int nprod, void* ws, size_t ws_bytes,
+                                tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ Max pooling
  * Replaces: nn.MaxPool2d(kernel_size=2, stride=2) (floor mode) in RCNN_base (torchvision

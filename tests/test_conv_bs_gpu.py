@@ -443,3 +443,24 @@ def test_pack_bs_bit_exact(Cout, Cin, dgrad):
     assert p.numel() == ref.numel()
     assert torch.equal(p, ref)
 
+
+
+@pytest.mark.parametrize("KS,N,Cin,Cout,H,W", [(1, 2, 256, 1024, 19, 38), (1, 2, 1024, 256, 19, 38),
+                                              (3, 2, 256, 256, 19, 38), (3, 1, 64, 72, 30, 41)])
+def test_bn_scale_folded_into_dgrad_and_wgrad(KS, N, Cin, Cout, H, W):
+    """A frozen BatchNorm's per-channel scale after the conv, folded into the dgrad (staged
+    weight for 1x1, tlod_conv_pack_bs_ex for 3x3) and the wgrad reduce
+    (tlod_conv_wgrad_bs_ex_f32): bit-identical to scaling the weight / the weight gradient
+    with a separate pass (ConvBNFunction's skipped-ReLU path, round 4)."""
+    from tlod.conv import conv_dgrad, conv_wgrad
+    g = torch.Generator().manual_seed(KS * 100 + Cin + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, KS, KS, generator=g) * (2.0 / (Cin * KS * KS)) ** 0.5).to(dev)
+    s = (torch.rand(Cout, generator=g) + 0.5).to(dev)
+    gy = torch.randn(N, Cout, H, W, generator=g).to(dev)
+    m = torch.relu(torch.randn(N, Cin, H, W, generator=g)).to(dev)
+    a = conv_dgrad(gy, w, math="bf16x6", mask=m, wscale=s)
+    b = conv_dgrad(gy, w * s.view(-1, 1, 1, 1), math="bf16x6", mask=m)
+    assert torch.equal(a, b)
+    dw = conv_wgrad(gy, x, KS, math="bf16x6", row_scale=s)
+    assert torch.equal(dw, conv_wgrad(gy, x, KS, math="bf16x6") * s.view(-1, 1, 1, 1))

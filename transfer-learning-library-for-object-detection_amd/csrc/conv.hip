@@ -1564,7 +1564,10 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 // packs the transposed, flipped operand (rows = input channels, inputs = output channels,
 // tap 8-s).
 __global__ void pack_bs_kernel(const float* __restrict__ Wt, unsigned short* __restrict__ P,
-                               int rows, int ins, int nchunks, int dgrad) {
+                               int rows, int ins, int nchunks, int dgrad,
+                               const float* __restrict__ oscale) {
+  // oscale (optional): weight[co] * oscale[co] per output channel co before the split (a
+  // frozen BatchNorm's scale after the conv, tlod_conv_pack_bs_ex)
   // one thread per (row o, chunk c, tap slot s): 8 input channels -> one 16-B store per plane
   const size_t rowlen = (size_t)nchunks * kBsKP;
   const size_t plane = (size_t)rows * rowlen;
@@ -1579,8 +1582,10 @@ __global__ void pack_bs_kernel(const float* __restrict__ Wt, unsigned short* __r
     for (int e = 0; e < 8; ++e) {
       const int in = c * 8 + e;
       v[e] = 0.f;
-      if (in < ins && s < 9)
+      if (in < ins && s < 9) {
         v[e] = dgrad ? Wt[((size_t)in * rows + o) * 9 + (8 - s)] : Wt[((size_t)o * ins + in) * 9 + s];
+        if (oscale != nullptr) v[e] *= oscale[dgrad ? in : o];
+      }
     }
     u32x4 sp[3];
     split8<3>(v, sp);
@@ -2039,17 +2044,31 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
 }
 
 // dW = (accumulate ? dW : 0) + sum_s slab[s], summed in split order (deterministic).
+// row_scale (optional, per output channel, row_len = Cin*KS*KS): dW = (accumulate ? dW : 0)
+// + row_scale[co] * sum_s slab[s] — a frozen BatchNorm's scale folded into the weight gradient
+// of the conv before it (tlod_conv_wgrad_bs_ex_f32).
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, size_t count,
-                                   float* __restrict__ out, int accumulate) {
+                                   float* __restrict__ out, int accumulate,
+                                   const float* __restrict__ row_scale, int row_len) {
   const size_t n4 = count / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
-    float4 s = accumulate ? reinterpret_cast<const float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // (the unscaled form keeps the round-3 order: the existing dW first, then the splits)
+    float4 s = accumulate && row_scale == nullptr ? reinterpret_cast<const float4*>(out)[i]
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
     // unrolled: eight split loads in flight, the adds still in split order
 #pragma unroll 8
     for (int k = 0; k < splits; ++k) {
       const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * count)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (row_scale != nullptr) {  // row_len is a multiple of 4 (checked by the caller)
+      const float r = row_scale[(4 * i) / (size_t)row_len];
+      s.x *= r; s.y *= r; s.z *= r; s.w *= r;
+      if (accumulate) {
+        const float4 o = reinterpret_cast<const float4*>(out)[i];
+        s.x = o.x + s.x; s.y = o.y + s.y; s.z = o.z + s.z; s.w = o.w + s.w;
+      }
     }
     reinterpret_cast<float4*>(out)[i] = s;
   }
@@ -2829,7 +2848,7 @@ extern "C" int tlod_conv_wgrad_f32(const float* dy, const float* x, float* dw, i
   if (st) return st;
   const size_t count = (size_t)Cout * Cin * KS * KS;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count / 4 + 255) / 256, 2048)),
-                     dim3(256), 0, s, slab, splits, count, dw, accumulate);
+                     dim3(256), 0, s, slab, splits, count, dw, accumulate, nullptr, 1);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }
@@ -2844,8 +2863,9 @@ namespace tlod {
 // csrc/wgrad_ws.hip: the warp-specialized 3x3 weight gradient (2D pixel-tile chunks)
 bool wgrad_ws_applies(int N, int Cin, int H, int W, int Cout, int KS, int nprod);
 size_t wgrad_ws_workspace(int N, int Cin, int H, int W, int Cout);
-int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int accumulate, int N,
-                    int Cin, int H, int W, int Cout, void* ws, size_t ws_bytes, hipStream_t s);
+int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int accumulate,
+                    const float* row_scale, int N, int Cin, int H, int W, int Cout, void* ws,
+                    size_t ws_bytes, hipStream_t s);
 int launch_db_reduce(const float* db_slab, int splits, int C, float* db, int accumulate,
                      hipStream_t s) {
   hipLaunchKernelGGL(db_reduce_kernel, dim3(div_up(C, 256)), dim3(256), 0, s, db_slab, splits, C,
@@ -2866,6 +2886,14 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
                                       int accumulate, int N, int Cin, int H, int W, int Cout,
                                       int KS, int nprod, void* ws, size_t ws_bytes,
                                       tlod_stream_t stream) {
+  return tlod_conv_wgrad_bs_ex_f32(dy, x, dw, db, accumulate, nullptr, N, Cin, H, W, Cout, KS,
+                                   nprod, ws, ws_bytes, stream);
+}
+
+extern "C" int tlod_conv_wgrad_bs_ex_f32(const float* dy, const float* x, float* dw, float* db,
+                                         int accumulate, const float* row_scale, int N, int Cin,
+                                         int H, int W, int Cout, int KS, int nprod, void* ws,
+                                         size_t ws_bytes, tlod_stream_t stream) {
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "bad shape");
   TLOD_CHECK_ARG((Cout * Cin * KS * KS) % 4 == 0, "Cout*Cin*KS*KS must be a multiple of 4");
   TLOD_CHECK_ARG(KS == 1 || KS == 3, "conv wgrad: only 1x1 and 3x3 kernels");
@@ -2875,7 +2903,7 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
   TLOD_CHECK_ARG((size_t)H * W < (1u << 21), "map too large");
   hipStream_t s = (hipStream_t)stream;
   if (wgrad_ws_applies(N, Cin, H, W, Cout, KS, nprod))
-    return wgrad_ws_launch(dy, x, dw, db, accumulate, N, Cin, H, W, Cout, ws, ws_bytes, s);
+    return wgrad_ws_launch(dy, x, dw, db, accumulate, row_scale, N, Cin, H, W, Cout, ws, ws_bytes, s);
   const int splits =
       with_wgrad_bs_cfg(N, Cin, H, W, Cout, KS, nprod, [&](auto cfg) { return cfg.splits(N, Cin, H, W, Cout); });
   if (ws_bytes < wgrad_bs_ws(splits, Cin, Cout, KS)) {
@@ -2893,7 +2921,8 @@ extern "C" int tlod_conv_wgrad_bs_f32(const float* dy, const float* x, float* dw
   if (st) return st;
   const size_t count = (size_t)Cout * Cin * KS * KS;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<size_t>((count / 4 + 255) / 256, 2048)),
-                     dim3(256), 0, s, slab, splits, count, dw, accumulate);
+                     dim3(256), 0, s, slab, splits, count, dw, accumulate, row_scale,
+                     Cin * KS * KS);
   TLOD_LAUNCH_CHECK();
   if (db) {
     hipLaunchKernelGGL(db_reduce_kernel, dim3(div_up(Cout, 256)), dim3(256), 0, s, db_slab, splits,
@@ -2945,13 +2974,18 @@ extern "C" size_t tlod_conv_pack_bs_bytes(int Cout, int Cin, int KS, int dgrad) 
 
 extern "C" int tlod_conv_pack_bs(const float* weight, int Cout, int Cin, int KS, int dgrad,
                                  void* packed, tlod_stream_t stream) {
+  return tlod_conv_pack_bs_ex(weight, nullptr, Cout, Cin, KS, dgrad, packed, stream);
+}
+
+extern "C" int tlod_conv_pack_bs_ex(const float* weight, const float* scale, int Cout, int Cin,
+                                    int KS, int dgrad, void* packed, tlod_stream_t stream) {
   TLOD_CHECK_ARG(Cout > 0 && Cin > 0 && weight && packed, "bad arguments");
   TLOD_CHECK_ARG(KS == 3, "split-bf16 conv: 3x3 only");
   const int rows = dgrad ? Cin : Cout, ins = dgrad ? Cout : Cin;
   const size_t plane = (size_t)rows * div_up(ins, 8) * 10;  // threads: (row, chunk, tap slot)
   hipLaunchKernelGGL(pack_bs_kernel, dim3((unsigned)std::min<size_t>((plane + 255) / 256, 4096)),
                      dim3(256), 0, (hipStream_t)stream, weight, (unsigned short*)packed, rows, ins,
-                     div_up(ins, 8), dgrad);
+                     div_up(ins, 8), dgrad, scale);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

@@ -77,9 +77,18 @@ struct Stager {
   int lim[IT];     // for the tail mask: K - k (KC) or R - r (MN)
   f32x4v r[IT], r2[IT];  // data slots 0 / 1 (mainloop's two-chunk prefetch uses both)
   unsigned mask[IT], mask2[IT];
+  // M/N-contiguous operands only: element (r, k) *= kscale[k] when staged (a frozen BN's
+  // scale on the conv weight's output channels, the 1x1 dgrad's K); nullptr: none
+  const float* kscale = nullptr;
+  int ktot = 0, kb[2] = {0, 0};
+
+  int tid0 = 0;
+  __device__ int tid_of(int i) const { return tid0 + i * kNT; }  // vector index of slot i
 
   __device__ void init(const float* P, int R, int K, int r0, int tid) {
     rsrc = make_buffer_rsrc(P, (unsigned)R * (unsigned)K * 4u);
+    ktot = K;
+    tid0 = tid;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int idx = tid + i * kNT;
@@ -101,6 +110,7 @@ struct Stager {
   __device__ void load(int kc, int R) {
     f32x4v* rr = S ? r2 : r;
     unsigned* mm = S ? mask2 : mask;
+    kb[S] = kc;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (KC) {
@@ -122,6 +132,11 @@ struct Stager {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = ((mm[i] >> e) & 1) ? rr[i][e] : 0.f;
+      if (!KC && kscale != nullptr) {  // uniform branch; k rows past K are zero already
+        const float sc = kscale[min(kb[S] + (tid_of(i) / LPR), ktot - 1)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= sc;
+      }
       unsigned sp[3][2];
       split4<NPL>(v, sp);
 #pragma unroll
@@ -560,6 +575,7 @@ struct ConvEpi {
   const float* residual;
   int relu;
   const float* mask = nullptr;  // y *= (mask > 0) last: a dgrad's previous-layer ReLU backward
+  const float* wscale = nullptr;  // 1x1 dgrad (w_layout 1): W[co][ci] * wscale[co] as staged
 };
 
 template <int NPL>
@@ -689,6 +705,7 @@ conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, C
     sb.init(X, N, C, H, W, img, p0, tid);
     mainloop<AK, 0, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, Cout, 0);
   } else {  // 1x1: B(p, c) = X[img][c][p], the image's map as an N-contiguous operand
+    if constexpr (AK == 0) sa.kscale = epi.wscale;
     Stager<0, NPL, kBN> sb;
     sb.init(X + (size_t)img * C * P, P, C, p0, tid);
     mainloop<AK, 0, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, Cout, P);
@@ -980,13 +997,15 @@ extern "C" size_t tlod_conv1x1_gemm_bs_workspace_bytes(int N, int Cin, int H, in
 
 extern "C" int tlod_conv1x1_gemm_bs_ex_f32(const float* x, const float* w, int w_layout,
                                            const float* scale, const float* bias,
-                                           const float* residual, const float* mask, float* y,
-                                           int N, int Cin, int H, int W, int Cout, int relu,
-                                           int nprod, void* ws, size_t ws_bytes,
-                                           tlod_stream_t stream) {
+                                           const float* residual, const float* mask,
+                                           const float* w_scale, float* y, int N, int Cin, int H,
+                                           int W, int Cout, int relu, int nprod, void* ws,
+                                           size_t ws_bytes, tlod_stream_t stream) {
   TLOD_CHECK_ARG(mask != y || mask == nullptr, "mask must not alias y");
+  TLOD_CHECK_ARG(w_scale == nullptr || w_layout == 1, "w_scale: the dgrad layout only");
   ConvEpi e{scale, bias, residual, relu};
   e.mask = mask;
+  e.wscale = w_scale;
   TLOD_CHECK_ARG(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0 && x && w && y, "bad arguments");
   TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
   TLOD_CHECK_ARG(w_layout == 0 || w_layout == 1, "w_layout must be 0 or 1");

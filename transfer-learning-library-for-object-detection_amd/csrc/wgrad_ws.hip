@@ -495,7 +495,8 @@ wgrad_ws_kernel(const float* __restrict__ G, const float* __restrict__ X,
 __global__ void __launch_bounds__(256) wgws_reduce_kernel(const float* __restrict__ slab,
                                                           float* __restrict__ dw, int splits,
                                                           int tiles_m, int tiles_c, int Cin,
-                                                          int Cout, int accumulate) {
+                                                          int Cout, int accumulate,
+                                                          const float* __restrict__ row_scale) {
   using namespace wgws;
   const int tiles = tiles_m * tiles_c;
   const int idx = blockIdx.x * 256 + threadIdx.x;  // float4 index within one split's slab
@@ -530,7 +531,8 @@ __global__ void __launch_bounds__(256) wgws_reduce_kernel(const float* __restric
     const int co = mt * BM + 32 * (w & 3) + 16 * i + 4 * g + e;
     if (co >= Cout) continue;
     float* d = dw + ((size_t)co * Cin + ci) * 9 + t;
-    *d = accumulate ? *d + sum[e] : sum[e];
+    const float v = row_scale != nullptr ? sum[e] * row_scale[co] : sum[e];
+    *d = accumulate ? *d + v : v;
   }
 }
 
@@ -590,8 +592,9 @@ size_t wgrad_ws_workspace(int N, int Cin, int H, int W, int Cout) {
 int launch_db_reduce(const float* db_slab, int splits, int C, float* db, int accumulate,
                      hipStream_t s);
 
-int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int accumulate, int N,
-                    int Cin, int H, int W, int Cout, void* ws, size_t ws_bytes, hipStream_t s) {
+int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int accumulate,
+                    const float* row_scale, int N, int Cin, int H, int W, int Cout, void* ws,
+                    size_t ws_bytes, hipStream_t s) {
   using namespace wgws;
   const WgwsPlan p = wgws_plan(N, Cin, H, W, Cout);
   if (ws_bytes < wgrad_ws_workspace(N, Cin, H, W, Cout)) {
@@ -616,7 +619,7 @@ int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int a
   TLOD_LAUNCH_CHECK();
   const int n4 = tiles * TILE_FLOATS / 4;
   hipLaunchKernelGGL(wgws_reduce_kernel, dim3((unsigned)div_up(n4, 256)), dim3(256), 0, s, slab, dw,
-                     p.splits, p.tiles_m, p.tiles_c, Cin, Cout, accumulate);
+                     p.splits, p.tiles_m, p.tiles_c, Cin, Cout, accumulate, row_scale);
   TLOD_LAUNCH_CHECK();
   if (db) return launch_db_reduce(db_slab, p.splits, Cout, db, accumulate, s);
   return kOk;

@@ -92,6 +92,7 @@ SIGNATURES = {
     "tlod_relu_bwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, P]),
     "tlod_conv_pack_bs_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "tlod_conv_pack_bs": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_conv_pack_bs_ex": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_conv_fwd_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
                                                     c_int]),
     "tlod_conv_fwd_bs_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -100,6 +101,8 @@ SIGNATURES = {
                                                       c_int]),
     "tlod_conv_wgrad_bs_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                        c_int, c_int, P, c_size_t, P]),
+    "tlod_conv_wgrad_bs_ex_f32": (c_int, [P, P, P, P, c_int, P, c_int, c_int, c_int, c_int,
+                                          c_int, c_int, c_int, P, c_size_t, P]),
     "tlod_conv3x3_direct_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "tlod_conv_dgrad_bs_mask_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                             P, c_size_t, P]),
@@ -116,7 +119,7 @@ SIGNATURES = {
                                                         c_int]),
     "tlod_conv1x1_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, P, c_size_t, P]),
-    "tlod_conv1x1_gemm_bs_ex_f32": (c_int, [P, P, c_int, P, P, P, P, P, c_int, c_int, c_int,
+    "tlod_conv1x1_gemm_bs_ex_f32": (c_int, [P, P, c_int, P, P, P, P, P, P, c_int, c_int, c_int,
                                             c_int, c_int, c_int, c_int, P, c_size_t, P]),
     "tlod_maxpool2x2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_maxpool2x2_relu_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),

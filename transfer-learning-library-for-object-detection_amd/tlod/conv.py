@@ -102,7 +102,8 @@ def _gemm1x1(KS, math, cin, cout):
             and os.environ.get("TLOD_CONV1X1_BS", "1") != "0")
 
 
-def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS=3, mask=None):
+def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS=3, mask=None,
+               wscale=None):
     N, Cin, H, W = x.shape
     y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
     b = bias.detach().contiguous() if bias is not None else None
@@ -118,15 +119,18 @@ def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS
                       "conv1x1_gemm_bs"))
     ws = _lib.workspace(wsb(N, Cin, H, W, Cout, w_layout, nprod), x.device, "conv")
     shape = (N, Cin, H, W, Cout, KS) if kind == "fwd" else (N, Cout, H, W, Cin, KS)
-    if mask is not None:  # 1x1 only: y *= (mask > 0) last (tlod_conv1x1_gemm_bs_ex_f32)
-        assert KS == 1 and mask.shape == y.shape, (KS, mask.shape, y.shape)
-        mk = mask.detach().contiguous()
+    if mask is not None or wscale is not None:
+        # 1x1 only (tlod_conv1x1_gemm_bs_ex_f32): y *= (mask > 0) last; the weight's output
+        # channels scaled by wscale as it is staged (dgrad layout)
+        assert KS == 1 and (mask is None or mask.shape == y.shape), (KS, y.shape)
+        mk = mask.detach().contiguous() if mask is not None else None
+        wsc = wscale.detach().contiguous() if wscale is not None else None
         _timed(kind, shape, lambda: _lib.check(
             L.tlod_conv1x1_gemm_bs_ex_f32(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc),
-                                          _lib.ptr(b), _lib.ptr(res), _lib.ptr(mk), _lib.ptr(y),
-                                          N, Cin, H, W, Cout, int(relu), nprod, _lib.ptr(ws),
-                                          ws.numel(), _lib.stream_of(x)), "conv1x1_gemm_bs_ex"),
-            math)
+                                          _lib.ptr(b), _lib.ptr(res), _lib.ptr(mk), _lib.ptr(wsc),
+                                          _lib.ptr(y), N, Cin, H, W, Cout, int(relu), nprod,
+                                          _lib.ptr(ws), ws.numel(), _lib.stream_of(x)),
+            "conv1x1_gemm_bs_ex"), math)
         return y
     _timed(kind, shape, lambda: _lib.check(
         fn(_lib.ptr(x), _lib.ptr(w), w_layout, _lib.ptr(sc), _lib.ptr(b), _lib.ptr(res),
@@ -164,13 +168,16 @@ def pack_bs(weight, dgrad):
     return _pack_bs(weight, dgrad)
 
 
-def _pack_bs(weight, dgrad):
+def _pack_bs(weight, dgrad, scale=None):
+    """scale (Cout, optional): pack weight[co] * scale[co] (tlod_conv_pack_bs_ex)."""
     Cout, Cin, KS, _ = weight.shape
     L = _lib.lib()
     p = torch.empty(L.tlod_conv_pack_bs_bytes(Cout, Cin, KS, int(dgrad)), dtype=torch.uint8,
                     device=weight.device)
-    _lib.check(L.tlod_conv_pack_bs(_lib.ptr(weight.detach().contiguous()), Cout, Cin, KS,
-                                   int(dgrad), _lib.ptr(p), _lib.stream_of(weight)), "pack_bs")
+    sc = scale.detach().contiguous() if scale is not None else None
+    _lib.check(L.tlod_conv_pack_bs_ex(_lib.ptr(weight.detach().contiguous()), _lib.ptr(sc), Cout,
+                                      Cin, KS, int(dgrad), _lib.ptr(p), _lib.stream_of(weight)),
+               "pack_bs")
     return p
 
 
@@ -266,25 +273,34 @@ def _conv_bs(x, wp, bias, relu, scale, residual, Cout, KS, math, kind):
     return y
 
 
-def conv_dgrad(g, weight, wd=None, math=None, mask=None, residual=None):
+def conv_dgrad(g, weight, wd=None, math=None, mask=None, residual=None, wscale=None):
     """Input gradient.  mask (the conv's input, when that is the previous conv's ReLU output):
     on the split-bf16 3x3 path and the split-bf16 1x1 GEMM the result is dx * (mask > 0) — the
     previous layer's ReLU backward done in this epilogue (tlod_conv_dgrad_bs_mask_f32,
     tlod_conv1x1_gemm_bs_ex_f32) — and it is tagged so that layer's backward skips its own pass
     (ConvFunction, ConvBNFunction); other paths ignore mask.  residual (1x1 GEMM path, or
     added here otherwise): a gradient summed into dx before the mask (a bottleneck's identity
-    shortcut)."""
+    shortcut).  wscale (Cout, optional): the gradient through weight * wscale[co] (a frozen
+    BatchNorm's scale after the conv) — applied as the 1x1 GEMM stages the weight or by the
+    3x3 pack, not as a pass over the weight."""
     g = g.contiguous()
     N, Cout, H, W = g.shape
     _, Cin, KS, _ = weight.shape
     math = conv_math() if math is None else math
-    if _gemm1x1(KS, math, Cout, Cin) and (mask is not None or residual is not None):
+    if _gemm1x1(KS, math, Cout, Cin) and (mask is not None or residual is not None or
+                                          wscale is not None):
         dx = _conv_gemm(g, weight.detach().contiguous(), 1, None, False, None, residual, Cin,
-                        math, "dgrad", KS=1, mask=mask)
+                        math, "dgrad", KS=1, mask=mask, wscale=wscale)
         if mask is not None:
             dx._tlod_relu_masked = (mask.data_ptr(), dx.data_ptr(), dx._version)
             STATS["masked_dgrad"] += 1
         return dx
+    if wscale is not None:
+        if _bs(KS, math) and not _gemm_conv(KS, math, Cin) and wd is None:
+            wd = _pack_bs(weight, True, wscale)
+        else:
+            weight = weight.detach() * wscale.view(-1, 1, 1, 1)
+            wd = None
     if residual is not None:
         return conv_dgrad(g, weight, wd, math).add_(residual)
     if mask is not None and _bs(KS, math) and not _gemm_conv(KS, math, Cin):
@@ -342,10 +358,11 @@ def wgrad_math():
     return m
 
 
-def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None, db=None):
+def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None, db=None, row_scale=None):
     """Weight gradient (into out when given).  db (Cout floats, optional): also the bias
     gradient sum_{n,h,w} g, from the same launch on the split-bf16 path (the f32 path adds
-    a reduction pass)."""
+    a reduction pass).  row_scale (Cout, optional): dW[co] scaled by row_scale[co] — in the
+    split-bf16 path's reduce (tlod_conv_wgrad_bs_ex_f32), else a pass over dW."""
     g = g.contiguous()
     x = x.contiguous()
     N, Cout, H, W = g.shape
@@ -358,11 +375,17 @@ def conv_wgrad(g, x, KS, out=None, accumulate=False, math=None, db=None):
         nprod = 6 if math == "bf16x6" else 3
         ws = _lib.workspace(L.tlod_conv_wgrad_bs_workspace_bytes(N, Cin, H, W, Cout, KS, nprod),
                             g.device, "wgrad")
+        rs = row_scale.detach().contiguous() if row_scale is not None else None
         _timed("wgrad", (N, Cin, H, W, Cout, KS), lambda: _lib.check(
-            L.tlod_conv_wgrad_bs_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db),
-                                     int(accumulate), N, Cin, H, W, Cout, KS, nprod, _lib.ptr(ws),
-                                     ws.numel(), _lib.stream_of(g)), "conv_wgrad_bs"), math)
+            L.tlod_conv_wgrad_bs_ex_f32(_lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db),
+                                        int(accumulate), _lib.ptr(rs), N, Cin, H, W, Cout, KS,
+                                        nprod, _lib.ptr(ws), ws.numel(), _lib.stream_of(g)),
+            "conv_wgrad_bs"), math)
         return dw
+    if row_scale is not None:
+        assert not accumulate
+        dw = conv_wgrad(g, x, KS, out, False, math, db)
+        return dw.mul_(row_scale.detach().view(-1, 1, 1, 1))
     if db is not None:
         relu_bwd_bias(g, None, want_db=True, db_out=db)
     ws = _lib.workspace(L.tlod_conv_wgrad_workspace_bytes(N, Cin, H, W, Cout, KS), g.device, "wgrad")
@@ -508,12 +531,10 @@ class ConvBNFunction(torch.autograd.Function):
             # masks conv1's gradient): the BN scale g = dy * scale folds into the dgrad weight
             # (W * scale per output channel) and the weight gradient's rows — no pass over dy
             STATS["relu_bwd_skipped"] += 1
-            s4 = scale.detach().view(-1, 1, 1, 1)
-            dx = conv_dgrad(dy, weight.detach() * s4, mask=mask, residual=res) if need_x else None
-            dw = None
-            if need_w:
-                dw = conv_wgrad(dy, x, weight.shape[2], out=grad_out(ctx.wparam))
-                dw.mul_(s4)
+            dx = (conv_dgrad(dy, weight, mask=mask, residual=res, wscale=scale)
+                  if need_x else None)
+            dw = (conv_wgrad(dy, x, weight.shape[2], out=grad_out(ctx.wparam), row_scale=scale)
+                  if need_w else None)
             return dx, dw, dy if need_res else None
         g, g_raw = relu_bwd_ex(dy, y if ctx.relu else None, scale, want_raw=need_res)
         dx = conv_dgrad(g, weight, mask=mask, residual=res) if need_x else None
