@@ -2111,6 +2111,8 @@ __global__ void __launch_bounds__(256) fwd_tail_reduce_kernel(
   const int co = mt * bm + ml;
   if (co >= Cout) return;
   float4 v = *reinterpret_cast<const float4*>(S + e0);
+  // unrolled: four split loads in flight, the adds in split order
+#pragma unroll 4
   for (int k = 1; k < ksplit; ++k) {
     const float4 u = *reinterpret_cast<const float4*>(S + k * stride + e0);
     v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;

@@ -430,6 +430,7 @@ __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
   const int m = mt * bm + e / kBN, n = nt * kBN + e % kBN;
   if (m >= M || n >= N) return;
   float4 v = *reinterpret_cast<const float4*>(S + e);
+#pragma unroll 4  // four split loads in flight, the adds in split order
   for (int k = 1; k < ksplit; ++k) {
     const float4 u = *reinterpret_cast<const float4*>(S + k * stride + e);
     v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
@@ -776,7 +777,8 @@ conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, C
 }
 
 // Tail tiles: Y = act(sum_s slab[s][tile] * scale + bias + residual), fixed split order.
-// One workgroup per (tail tile, 1024 elements).
+// One workgroup per (tail tile, 1024 elements); a thread takes 4 consecutive pixels of one
+// channel (16-B loads per split piece, four pieces in flight).
 __global__ void __launch_bounds__(256) conv_tail_reduce_kernel(
     const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tiles_m,
     int tiles_n, int Cout, int P, ConvEpi epi, float* __restrict__ Y) {
@@ -789,19 +791,29 @@ __global__ void __launch_bounds__(256) conv_tail_reduce_kernel(
   const int img = t / tiles_n;
   const size_t stride = (size_t)n_tail * tile_elems;
   const float* S = slab + (size_t)ti * tile_elems;
-  const int e0 = (blockIdx.x % per_tile) * 1024;
-  for (int e = e0 + threadIdx.x; e < e0 + 1024; e += 256) {
-    const int co = mt * bm + e / kBN, p = nt * kBN + e % kBN;
-    if (co >= Cout || p >= P) continue;
-    float v = S[e];
-    for (int k = 1; k < ksplit; ++k) v += S[k * stride + e];
+  const int e = (blockIdx.x % per_tile) * 1024 + 4 * threadIdx.x;
+  const int co = mt * bm + e / kBN, p0 = nt * kBN + e % kBN;
+  if (co >= Cout || p0 >= P) return;
+  float4 v = *reinterpret_cast<const float4*>(S + e);
+#pragma unroll 4
+  for (int k = 1; k < ksplit; ++k) {
+    const float4 u = *reinterpret_cast<const float4*>(S + k * stride + e);
+    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  }
+  const float vv[4] = {v.x, v.y, v.z, v.w};
+  const float sc = epi.scale ? epi.scale[co] : 1.f, bi = epi.bias ? epi.bias[co] : 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = p0 + q;
+    if (p >= P) break;
     const size_t idx = ((size_t)img * Cout + co) * P + p;
-    if (epi.scale) v *= epi.scale[co];
-    if (epi.bias) v += epi.bias[co];
-    if (epi.residual) v += epi.residual[idx];
-    if (epi.relu) v = fmaxf(v, 0.f);
-    if (epi.mask) v = epi.mask[idx] > 0.f ? v : 0.f;
-    Y[idx] = v;
+    float x = vv[q];
+    if (epi.scale) x *= sc;
+    if (epi.bias) x += bi;
+    if (epi.residual) x += epi.residual[idx];
+    if (epi.relu) x = fmaxf(x, 0.f);
+    if (epi.mask) x = epi.mask[idx] > 0.f ? x : 0.f;
+    Y[idx] = x;
   }
 }
 

@@ -40,7 +40,13 @@ def _timed(kind, shape, fn, math="f32"):
         N, Cin, H, W, Cout, KS = shape
         flops = 2.0 * N * H * W * Cout * Cin * KS * KS
     kind = f"{kind}/{math}"
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # events from bench.py's pre-created pool when it has one (creating two events per
+    # launch cost the host ~10 us per launch inside the timed region)
+    pool = getattr(PROFILE, "pool", None)
+    if pool:
+        s, e = pool.pop()
+    else:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     r = fn()
     e.record()
