@@ -1285,7 +1285,12 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
   const int aoffL = a_lane + 16 * (8 + (lane >> 5)) + hb, boffL = tap_c(8) + hb;
 
   f32x4 acc[RB][CB];
+  // TLOD_WS_PRIO: 1 = the younger half of the MFMA waves (4-7) at priority 1 for the whole
+  // kernel; 2 = priority 1 around every k-step's MFMA cluster (cdna_hip_programming.md T5)
+  if (TLOD_WS_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
+    __builtin_amdgcn_s_setprio(1);
   auto step16 = [&](int ao, int bo) {
+    if (TLOD_WS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     u32x4 a[RB][3];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -1301,6 +1306,7 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) bs_mac16<NP>(acc[rb][cb], a[rb], b, mfma16_bf16);
     }
+    if (TLOD_WS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   };
   auto step8 = [&](int ao, int bo) {
     u32x2 a[RB][3];

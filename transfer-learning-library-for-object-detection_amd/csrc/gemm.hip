@@ -34,6 +34,14 @@ namespace {
 #ifndef TLOD_MID_STORE
 #define TLOD_MID_STORE 1  // stage the next chunk mid-MFMA-phase (see conv.hip)
 #endif
+// 1: priority 1 around each chunk's MFMA cluster (cdna_hip_programming.md T5): fc6 fwd /
+// wgrad -1.2% / -2.4%, fc7 wgrad -2.5% (two interleaved pairs, one lease).  The same around
+// the ws conv's and wgrad_ws's k-steps (TLOD_WS_PRIO=2, TLOD_WGWS_MPRIO=2) made them slower
+// (conv3_3 dgrad 0.399 -> 0.411 ms); the static form (waves 4-7 at priority 1, =1) measured
+// within noise.
+#ifndef TLOD_GEMM_PRIO
+#define TLOD_GEMM_PRIO 1
+#endif
 #ifndef TLOD_GEMM_DEPTH2  // two chunks of loads in flight (mainloop, MI <= 2 tiles)
 #define TLOD_GEMM_DEPTH2 1
 #endif
@@ -263,6 +271,7 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
         sa.template load<S>((c_begin + j + 3) * kTK, Ra);
         sb.template load<S>((c_begin + j + 3) * kTK, Rb);
       };
+      if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
       u32x4 b[kNJ][3];
 #pragma unroll
       for (int jj = 0; jj < kNJ; ++jj)
@@ -280,6 +289,7 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
         for (int jj = 0; jj < kNJ; ++jj)
           bs_mac<NP>(acc[i][jj], a[0], a[1], a[2], b[jj][0], b[jj][1], b[jj][2]);
       }
+      if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
       __syncthreads();
     };
     const std::integral_constant<int, 0> S0;
@@ -327,6 +337,7 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
       for (int j = 0; j < 2 * kNJ; ++j) bs_mac16x16<NP>(acc[i][j], a, b[j]);
     }
 #else
+    if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
     u32x4 b[kNJ][3];
 #pragma unroll
     for (int j = 0; j < kNJ; ++j)
@@ -345,6 +356,7 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
         bs_mac<NP>(acc[i][j], a[0], a[1], a[2], b[j][0], b[j][1], b[j][2]);
       }
     }
+    if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
 #endif
     if (!TLOD_MID_STORE && more) store(smem + ((it + 1) & 1) * BUF);
     __syncthreads();

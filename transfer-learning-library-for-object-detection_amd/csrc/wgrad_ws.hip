@@ -73,6 +73,9 @@ static_assert(A_ITEMS % (NPW * 64) == 0, "A staging");
 #ifndef TLOD_WGWS_PRIO  // s_setprio of the producer waves (0: default)
 #define TLOD_WGWS_PRIO 0
 #endif
+#ifndef TLOD_WGWS_MPRIO  // MFMA waves: 1 = waves 4-7 at priority 1; 2 = per k-step cluster
+#define TLOD_WGWS_MPRIO 0
+#endif
 #ifndef TLOD_WGWS_STAMPS
 #define TLOD_WGWS_STAMPS 0
 #endif
@@ -356,7 +359,10 @@ wgrad_ws_kernel(const float* __restrict__ G, const float* __restrict__ X,
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if (TLOD_WGWS_MPRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
+    __builtin_amdgcn_s_setprio(1);
   auto kstep = [&](const unsigned char* buf, int a_off, int b_off) {
+    if (TLOD_WGWS_MPRIO == 2) __builtin_amdgcn_s_setprio(1);
     u32x4 a[2][3];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -396,6 +402,7 @@ wgrad_ws_kernel(const float* __restrict__ G, const float* __restrict__ X,
         }
       }
     }
+    if (TLOD_WGWS_MPRIO == 2) __builtin_amdgcn_s_setprio(0);
   };
   // B staging by the MFMA waves (TLOD_WGWS_BSPLIT): lane tid < 432 owns one (octet,
   // position) item of the patch; chunk j's 8 channel values are loaded two chunks ahead
