@@ -23,6 +23,7 @@
  *                          warp-specialized pixel-tile kernel;
  *   TLOD_WG1X1_TILE=256|128  1x1 split-bf16 weight gradient tile (default: cost model);
  *   TLOD_GEMM_WS=1         bf16x6 GEMMs on the warp-specialized kernel (csrc/gemm_ws.hip);
+ *   TLOD_CONV_KSPLIT_MAX=n, TLOD_WGWS_SPLIT_MAX=n  caps on the split-K planners (A/B only);
  *   TLOD_CONV_WS=0, TLOD_WS_MINCIN=n, TLOD_WS_FLEX=0, TLOD_WS_PERSIST=1, TLOD_CONV_BAND=0,
  *   TLOD_CONV_FWD_CK=4, TLOD_CONV_WGRAD_TH=2
  *                          split-bf16 / f32 conv forward tilings (see csrc/conv.hip);

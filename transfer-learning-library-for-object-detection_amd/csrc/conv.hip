@@ -2311,7 +2311,8 @@ static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int n
   if (!allow_split) return p;
   const double tile_s = tile_flops / (157.3e12 * 0.65 / slots);
   double best = (double)((T + slots - 1) / slots) * tile_s;
-  const int kmax = std::min(8, nchunks / 2);
+  static const int kcap = tune_knob("TLOD_CONV_KSPLIT_MAX", 8);  // A/B: cap the K split
+  const int kmax = std::min({8, kcap, nchunks / 2});
   const long long q = T / slots;
   for (int k = 2; k <= kmax; ++k) {
     const int cps = div_up(div_up(nchunks, k), cps_align) * cps_align;

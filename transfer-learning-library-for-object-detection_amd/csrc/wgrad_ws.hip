@@ -574,7 +574,11 @@ static WgwsPlan wgws_plan(int N, int Cin, int H, int W, int Cout) {
   const double tile_bytes = (double)TILE_FLOATS * 4.0;
   int best = 1;
   double best_t = 1e30;
-  for (int sp = 1; sp <= std::min(256, chunks); ++sp) {
+  static const int spcap = [] {  // A/B: cap the split count (TLOD_WGWS_SPLIT_MAX)
+    const char* v = getenv("TLOD_WGWS_SPLIT_MAX");
+    return v && *v ? std::max(1, atoi(v)) : 256;
+  }();
+  for (int sp = 1; sp <= std::min({256, spcap, chunks}); ++sp) {
     const int cps = div_up(chunks, sp);
     const int esp = div_up(chunks, cps);
     const long long rounds = ((long long)tiles * esp + slots - 1) / slots;
