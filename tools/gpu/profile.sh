@@ -1,5 +1,5 @@
 # Round profile of HEAD: rocprofv3 kernel stats of the bench command, PMC HBM traffic passes
-# (FETCH_SIZE, WRITE_SIZE: separate runs), the conv3_3 backward microbench and its kernel
+# (FETCH_SIZE, WRITE_SIZE: separate runs; 14 steps per bench run = 3 warmup + 1 launch-count probe + 10 timed), the conv3_3 backward microbench and its kernel
 # stats, per-shape conv timings.  usage: bash tools/gpu/profile.sh OUTDIR [PROFILE_DIR]
 set -e
 O=$1; P=${2:-}
@@ -12,7 +12,7 @@ B="python3 bench.py --steps 10 --warmup 3 --cpu-baseline-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- $B > $O/bench_rocprof.json 2> $O/stats.err
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $B > /dev/null 2> $O/fetch.err
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $B > /dev/null 2> $O/write.err
-python3 tools/pmc_traffic.py $O/fetch $O/write 13 $O/traffic.json > /dev/null || true
+python3 tools/pmc_traffic.py $O/fetch $O/write 14 $O/traffic.json > /dev/null || true
 timeout -k 10 120 python3 tools/bench_conv.py --math bf16x6 > $O/conv33.json 2> $O/conv33.err
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/conv33_stats -o run -- python3 tools/bench_conv.py --math bf16x6 > $O/conv33_rocprof.json 2> $O/conv33_stats.err
 TLOD_BENCH_SHAPES=1 timeout -k 10 200 $B > $O/bench_shapes.json 2> $O/bench_shapes.err
