@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <unordered_map>
 
 namespace tlod {
 
@@ -59,9 +60,9 @@ constexpr int kPitchK = 48;    // [row][16 k] images
 // k rows x 2 column halves); 16x16: rows 8 banks apart (8 k rows x 16 columns)
 constexpr int kPitchMN = TLOD_GEMM_MF16 ? 544 : 576;
 
-template <int KC>
-struct Img {  // one operand's LDS image per plane
-  static constexpr int PLANE = KC ? 256 * kPitchK : kTK * kPitchMN;
+template <int KC, int R = 256>
+struct Img {  // one operand's LDS image per plane (K-contiguous: R rows; M/N-contiguous: 256)
+  static constexpr int PLANE = KC ? R * kPitchK : kTK * kPitchMN;
 };
 
 __device__ __forceinline__ uint2 ds_read_tr16(const unsigned char* p) {
@@ -149,7 +150,7 @@ struct Stager {
       split4<NPL>(v, sp);
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl)
-        *reinterpret_cast<uint2*>(img + pl * Img<KC>::PLANE + lds[i]) = make_uint2(sp[pl][0], sp[pl][1]);
+        *reinterpret_cast<uint2*>(img + pl * Img<KC, RT>::PLANE + lds[i]) = make_uint2(sp[pl][0], sp[pl][1]);
     }
   }
 };
@@ -231,7 +232,7 @@ template <int AK, int BK, int NP, int MI, class SA, class SB>
 __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_begin,
                                          int c_end, unsigned char* smem, int Ra, int Rb) {
   constexpr int NPL = NP == 6 ? 3 : 2;
-  constexpr int A_PL = Img<AK>::PLANE, B_PL = Img<BK>::PLANE;
+  constexpr int A_PL = Img<AK, kWM * MI * 32>::PLANE, B_PL = Img<BK, kBN>::PLANE;
   constexpr int BUF = NPL * (A_PL + B_PL);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / kWN, wn = wid % kWN;
@@ -464,10 +465,14 @@ __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
   }
 }
 
+// resident workgroups of a kernel chip-wide, cached per kernel (the instantiations share one
+// function-pointer type, so a per-type static would mix kernels of different occupancy)
 template <typename K>
 int slots_of(K kern, size_t lds) {
-  static int cached = 0;
-  if (cached) return cached;
+  static std::unordered_map<const void*, int> cache;
+  const auto hit = cache.find((const void*)kern);
+  if (hit != cache.end()) return hit->second;
+  int& cached = cache[(const void*)kern];
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -475,7 +480,7 @@ int slots_of(K kern, size_t lds) {
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kNT, lds) != hipSuccess ||
       per_cu < 1 || cus < 1) {
     (void)hipGetLastError();
-    return 256;
+    return cached = 256;
   }
   return cached = per_cu * cus;
 }
@@ -513,7 +518,7 @@ template <int AK, int BK, int NP, int MI>
 struct Gemm {
   static constexpr int NPL = NP == 6 ? 3 : 2;
   static constexpr int kBM = kWM * MI * 32;
-  static constexpr size_t kLds = 2 * NPL * (Img<AK>::PLANE + Img<BK>::PLANE);
+  static constexpr size_t kLds = 2 * NPL * (Img<AK, kBM>::PLANE + Img<BK>::PLANE);
   static TailPlan plan(int M, int N, int K) {
     const int slots = slots_of(gemm_bs_kernel<AK, BK, NP, MI>, kLds);
     const int tiles = div_up(M, kBM) * div_up(N, kBN);
@@ -676,8 +681,15 @@ struct Im2colStager {
 // Schedule: the first dp_tiles tiles (whole rounds of the resident slots) run over the full
 // K; the remaining tail tiles, which would leave most of the chip idle in a last partial
 // round, are split over K into ksplit pieces written to fixed slabs and reduced in order.
+// MI = 1 (64-row tiles, 74 KB of LDS since the K-contiguous image is sized by the tile rows):
+// two workgroups per CU when the registers fit 128 (TLOD_CONV1X1_OCC2=1)
+#ifndef TLOD_CONV1X1_OCC2
+#define TLOD_CONV1X1_OCC2 1
+#endif
 template <int AK, int NP, int MI, int KS>
-__global__ void __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ void __launch_bounds__(kNT)
+    __attribute__((amdgpu_waves_per_eu(TLOD_CONV1X1_OCC2 && MI == 1 && AK == 1 ? 4 : 2,
+                                       TLOD_CONV1X1_OCC2 && MI == 1 && AK == 1 ? 4 : 2)))
 conv_gemm_bs_kernel(const float* __restrict__ X, const float* __restrict__ Wt, ConvEpi epi,
                     float* __restrict__ Y, float* __restrict__ slab, int N, int C, int H, int W,
                     int Cout, int tiles_m, int tiles_n, int dp_tiles, int ksplit,
@@ -834,7 +846,7 @@ template <int AK, int NP, int MI, int KS = 3>
 struct ConvGemm {
   static constexpr int NPL = NP == 6 ? 3 : 2;
   static constexpr int kBM = kWM * MI * 32;
-  static constexpr size_t kLds = 2 * NPL * (Img<AK>::PLANE + Img<0>::PLANE);
+  static constexpr size_t kLds = 2 * NPL * (Img<AK, kBM>::PLANE + Img<0>::PLANE);
   static TailPlan plan(int N, int C, int H, int W, int Cout) {
     const int slots = slots_of(conv_gemm_bs_kernel<AK, NP, MI, KS>, kLds);
     const int tiles = div_up(Cout, kBM) * div_up(H * W, kBN) * N;
