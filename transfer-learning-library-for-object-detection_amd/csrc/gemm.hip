@@ -43,6 +43,12 @@ namespace {
 #ifndef TLOD_GEMM_PRIO
 #define TLOD_GEMM_PRIO 1
 #endif
+#ifndef TLOD_GEMM_DEPTH3  // three chunks of loads in flight (64-row dgrad tiles, see mainloop)
+#define TLOD_GEMM_DEPTH3 0
+#endif
+#ifndef TLOD_CONV1X1_OCC2  // (see conv_gemm_bs_kernel)
+#define TLOD_CONV1X1_OCC2 1
+#endif
 #ifndef TLOD_GEMM_DEPTH2  // two chunks of loads in flight (mainloop, MI <= 2 tiles)
 #define TLOD_GEMM_DEPTH2 1
 #endif
@@ -84,12 +90,12 @@ struct Stager {
   int off[IT];     // element offset of this lane's 4-vector at chunk 0 (or -1: dead)
   int lds[IT];     // byte offset inside one plane image (-1: no slot)
   int lim[IT];     // for the tail mask: K - k (KC) or R - r (MN)
-  f32x4v r[IT], r2[IT];  // data slots 0 / 1 (mainloop's two-chunk prefetch uses both)
-  unsigned mask[IT], mask2[IT];
+  f32x4v r[IT], r2[IT], r3[IT];  // data slots 0 / 1 / 2 (mainloop's prefetch depth)
+  unsigned mask[IT], mask2[IT], mask3[IT];
   // M/N-contiguous operands only: element (r, k) *= kscale[k] when staged (a frozen BN's
   // scale on the conv weight's output channels, the 1x1 dgrad's K); nullptr: none
   const float* kscale = nullptr;
-  int ktot = 0, kb[2] = {0, 0};
+  int ktot = 0, kb[3] = {0, 0, 0};
 
   int tid0 = 0;
   __device__ int tid_of(int i) const { return tid0 + i * kNT; }  // vector index of slot i
@@ -117,8 +123,8 @@ struct Stager {
   }
   template <int S = 0>
   __device__ void load(int kc, int R) {
-    f32x4v* rr = S ? r2 : r;
-    unsigned* mm = S ? mask2 : mask;
+    f32x4v* rr = S == 2 ? r3 : S ? r2 : r;
+    unsigned* mm = S == 2 ? mask3 : S ? mask2 : mask;
     kb[S] = kc;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -133,8 +139,8 @@ struct Stager {
   }
   template <int S = 0>
   __device__ void store(unsigned char* img) const {
-    const f32x4v* rr = S ? r2 : r;
-    const unsigned* mm = S ? mask2 : mask;
+    const f32x4v* rr = S == 2 ? r3 : S ? r2 : r;
+    const unsigned* mm = S == 2 ? mask3 : S ? mask2 : mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (lds[i] < 0) continue;
@@ -244,6 +250,67 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
 #pragma unroll
       for (int r = 0; r < kAccRegs; ++r) acc[i][j][r] = 0.f;
 
+  if constexpr (TLOD_GEMM_DEPTH3 && MI == 1 && !(TLOD_CONV1X1_OCC2 && AK == 1)) {
+    // Three chunks in flight (the depth-2 scheme below with a third register slot): chunk k
+    // of the range lives in slot k % 3 from its load until its split + store; iteration j
+    // stores chunk j + 1 and loads chunk j + 4 into the freed slot.  64-row tiles only: the
+    // 128-row ones spill with a third slot, and the 64-row forward tile runs two workgroups
+    // per CU in a 128-register budget.
+    const int n = c_end - c_begin;
+    sa.template load<0>(c_begin * kTK, Ra);
+    sb.template load<0>(c_begin * kTK, Rb);
+    sa.template load<1>((c_begin + 1) * kTK, Ra);
+    sb.template load<1>((c_begin + 1) * kTK, Rb);
+    sa.template load<2>((c_begin + 2) * kTK, Ra);
+    sb.template load<2>((c_begin + 2) * kTK, Rb);
+    sa.template store<0>(smem);
+    sb.template store<0>(smem + NPL * A_PL);
+    sa.template load<0>((c_begin + 3) * kTK, Ra);
+    sb.template load<0>((c_begin + 3) * kTK, Rb);
+    __syncthreads();
+    auto iter = [&](auto slc, int j) {
+      constexpr int S = decltype(slc)::value;  // slot of chunk j + 1
+      const unsigned char* buf = smem + (j & 1) * BUF;
+      unsigned char* nbuf = smem + ((j + 1) & 1) * BUF;
+      auto mid = [&]() {
+        sa.template store<S>(nbuf);
+        sb.template store<S>(nbuf + NPL * A_PL);
+        sa.template load<S>((c_begin + j + 4) * kTK, Ra);
+        sb.template load<S>((c_begin + j + 4) * kTK, Rb);
+      };
+      if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+      u32x4 b[kNJ][3];
+#pragma unroll
+      for (int jj = 0; jj < kNJ; ++jj)
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          b[jj][pl] = read_operand<BK>(buf + NPL * A_PL + pl * B_PL, wn * kNJ * 32 + jj * 32, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if (i == MI / 2) mid();
+        u32x4 a[3];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          a[pl] = read_operand<AK>(buf + pl * A_PL, wm * MI * 32 + i * 32, lane);
+#pragma unroll
+        for (int jj = 0; jj < kNJ; ++jj)
+          bs_mac<NP>(acc[i][jj], a[0], a[1], a[2], b[jj][0], b[jj][1], b[jj][2]);
+      }
+      if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+      __syncthreads();
+    };
+    const std::integral_constant<int, 0> S0;
+    const std::integral_constant<int, 1> S1;
+    const std::integral_constant<int, 2> S2;
+    for (int j = 0; j < n; j += 3) {
+      iter(S1, j);
+      if (j + 1 >= n) break;
+      iter(S2, j + 1);
+      if (j + 2 >= n) break;
+      iter(S0, j + 2);
+    }
+    return;
+  }
   if constexpr (TLOD_GEMM_DEPTH2 && MI <= 2) {
     // Two chunks in flight: chunk j of the range sits in data slot j & 1 of the stagers from
     // its load until its split + store, half way through chunk j - 1's MFMAs; the store then
