@@ -374,9 +374,9 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
 
 // ======================================================================= split-bf16 forward
 // The same implicit GEMM on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32-input
-// rate) with every f32 operand split exactly into three bf16 terms (round-to-nearest),
-// x = hi + mid + lo (hi keeps the top 8 mantissa bits, mid the next 8, lo the last 8; the
-// remainders are exact in f32).  NP = 6 accumulates lo*hi, mid*mid, hi*lo, mid*hi, hi*mid,
+// rate) with every f32 operand split exactly into three bf16 terms, x = hi + mid + lo
+// (hi truncated, mid and lo round-to-nearest-even: hi keeps the top 8 mantissa bits, mid
+// the next 8, lo the last 8; the remainders are exact in f32).  NP = 6 accumulates lo*hi, mid*mid, hi*lo, mid*hi, hi*mid,
 // hi*hi (the dropped terms are < 2^-24 relative: f32-level error; measured normwise error
 // vs fp64 ~1e-7, the same as the f32-input MFMA path); NP = 3 keeps the last three
 // (~5e-6).  Products of bf16 pairs are exact in the f32 accumulator.
