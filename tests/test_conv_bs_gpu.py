@@ -32,6 +32,8 @@ SHAPES = [  # N, Cin, Cout, H, W
     # 150 x 300, 13 x 39 at 75 x 150, 19 x 26 at 37 x 75, 2 x 158 rows, blocks wrapping rows
     (2, 256, 256, 150, 300), (1, 128, 136, 75, 150), (1, 256, 64, 37, 75), (1, 128, 128, 2, 700),
     (1, 144, 128, 61, 9),
+    # round 5 staging layout: 30 x 17 tiles (row pitch TW + 16) at 150 x 250, 4 x 125 at 75 x 125
+    (1, 128, 136, 150, 250), (1, 136, 128, 75, 125),
     # stream-K tail (plan_stream_k: conv5 / RPN maps, 96 tiles over 256 slots), with an odd
     # chunk count (the lone last chunk in the last piece of each tile)
     (2, 512, 512, 37, 75), (2, 520, 512, 38, 75),

@@ -54,14 +54,30 @@ def main():
     out["wgrad_ms"] = timeit(lambda: tc.conv_wgrad(g, x, 3, math=m), a.iters)
     if m != "f32":
         out["wgrad_f32_ms"] = timeit(lambda: tc.conv_wgrad(g, x, 3, math="f32"), a.iters)
+    # the backward as the training step issues it: dgrad on the current stream, wgrad on a
+    # side stream (independent: dgrad reads dY and W, wgrad dY and X), wall clock of the pair
+    side = torch.cuda.Stream()
+    dw = torch.empty_like(w)
+
+    def pair():
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(side):
+            side.wait_event(ev)
+            tc.conv_wgrad(g, x, 3, out=dw, math=m)
+        tc.conv_dgrad(g, w, wd=wd, math=m)
+        torch.cuda.current_stream().wait_stream(side)
+    out["bwd_pair_ms"] = timeit(pair, a.iters)
     for k in ("fwd", "dgrad", "wgrad"):
         out[k + "_tflops"] = flop / (out[k + "_ms"] * 1e-3) / 1e12
     bwd = out["dgrad_ms"] + out["wgrad_ms"]
     out["bwd_gflop"] = 2 * flop / 1e9
     out["bwd_tflops"] = 2 * flop / (bwd * 1e-3) / 1e12
+    out["bwd_pair_tflops"] = 2 * flop / (out["bwd_pair_ms"] * 1e-3) / 1e12
     out["bwd_frac_f32_mfma_peak"] = out["bwd_tflops"] / 157.3
     if m != "f32":  # f32-equivalent peak of the split products
         out["bwd_frac_split_peak"] = out["bwd_tflops"] / (2516.6 / int(m[-1]))
+        out["bwd_pair_frac_split_peak"] = out["bwd_pair_tflops"] / (2516.6 / int(m[-1]))
     if a.torch:
         xr = x.clone().requires_grad_(True)
         wr = w.clone().requires_grad_(True)

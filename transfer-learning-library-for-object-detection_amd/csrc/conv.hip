@@ -717,134 +717,58 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
 }
 
 // ------------------------------------------------------------ warp-specialized variant
-// conv_fwd_bs_kernel's tile (64 output channels x 16 x 32 pixels) and K order, with
+// conv_fwd_bs_kernel's tile (64 output channels x TH x TW <= 512 pixels) and K order, with
 //  * the staging on kProdWaves extra producer waves (one per SIMD): the 8 MFMA waves only
 //    read LDS fragments and issue MFMAs, so the global-load waits, the split VALU and the
 //    LDS stores of the next chunk overlap the other waves' MFMAs instead of stalling both
 //    waves of a SIMD at once;
 //  * 16x16x32 MFMAs (v_mfma_f32_16x16x32_bf16): the chip holds a higher clock on this shape
-//    than on 32x32x16 for the same work (measured 2.10 vs 1.95 GHz on conv3_3);
-//  * persistent workgroups: a workgroup walks work items (whole tiles, then split-K pieces)
-//    b, b + G, ..., so the producers stage the next item's first chunks while the MFMA
-//    waves run the previous item's epilogue (one workgroup per CU: nothing else overlaps it).
-// Per chunk pair (chunk c in LDS buffer 0, c+1 in buffer 1; 18 (tap, 8-channel) units =
-// four 16x16x32 steps of 4 units + one 16x16x16 step of 2):
-//   steps 0-1   producers store chunk c+1 into buffer 1 (all but an item's first pair) and
-//               load chunk c+2
-//   barrier     (chunk c+1 visible)
-//   step 2      units 8..11: straddles the buffers
-//   barrier     (buffer 0 retired)
-//   steps 3-4   producers store chunk c+2 into buffer 0 and load chunk c+3
-//   barrier
+//    than on 32x32x16 for the same work (measured 2.10 vs 1.95 GHz on conv3_3).
+// One work item per workgroup: a whole tile, or one split-K piece of a tail tile (an
+// exiting workgroup's output stores drain while the next one stages; a persistent variant
+// measured slower, round 3).  K is walked in frames of four chunks (chunks c, c+2 in LDS
+// buffer 0, c+1, c+3 in buffer 1; 36 (tap, 8-channel) units = nine 16x16x32 k-steps), then
+// chunk pairs (18 units = four 16x16x32 steps + one 16x16x16 step), then a lone chunk.
 // Producers and MFMA waves run separate loops with the same barrier sequence, so neither
 // carries the other's registers (the kernel fits 3 waves per SIMD).
 constexpr int kProdWaves = 4;
 
-// Diagnostic build only (TLOD_WS_STAMPS=1; never in the shipped library): per-wave sums of
-// s_memtime cycles per pipeline segment of the warp-specialized loop, for blocks < 256,
-// read back with tlod_debug_ws_stamps.  Segment k = cycles from stamp k-1 to stamp k.
-#ifndef TLOD_WS_STAMPS
-#define TLOD_WS_STAMPS 0
-#endif
-// producer loads: 1 = flat global loads (invalid elements read g_zero), 0 = raw buffer
-// loads (invalid elements read past the range: 0)
-#ifndef TLOD_WS_FLAT
-#define TLOD_WS_FLAT 2
-#endif
-#ifndef TLOD_WS_ROT
-#define TLOD_WS_ROT 1
-#endif
-#ifndef TLOD_WS_NOSTORE
-#define TLOD_WS_NOSTORE 0
-#endif
-#ifndef TLOD_WS_FRAME  // four-chunk frames of nine 16x16x32 steps (0: chunk pairs only)
-#define TLOD_WS_FRAME 1
-#endif
-#ifndef TLOD_WS_DEPTH2  // producers two chunks ahead in registers (one-item mode)
-#define TLOD_WS_DEPTH2 1
-#endif
-// TLOD_WS_FLAGS=1 (one-item mode): producers and MFMA waves hand the two LDS buffers over
-// through counters in LDS instead of workgroup barriers — the producers store chunk j into
-// buffer j & 1 once every MFMA wave has retired chunk j - 2 from it and count it ready; an
-// MFMA wave waits only for the chunk its next k-step reads.  Measured slower (round 4,
-// conv3_3 shape, one lease: fwd 0.50 vs 0.47 ms, dgrad 0.447 vs 0.408): the MFMA waves drift
-// apart, the slowest one gates the producers' refill of a buffer, and with two buffers the
-// refill window shrinks (MFMA waves 26% and producers 67% of their cycles in the waits).
-#ifndef TLOD_WS_FLAGS
-#define TLOD_WS_FLAGS 0
-#endif
-// counter wait with a bounded spin: a miscounted protocol ends the kernel (wrong results,
-// caught by the tests) instead of hanging the GPU
-__device__ __forceinline__ void ws_wait_ge(const int* ctr, int target) {
-  for (int it = 0; it < (1 << 22); ++it) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");  // the reads that follow stay behind the poll
-}
-// one add per wave, after all of the wave's LDS operations so far have completed (LDS is
-// one coherent memory: a wave that sees the count sees the data / the retired reads)
-__device__ __forceinline__ void ws_signal(int* ctr) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-#if TLOD_WS_STAMPS
-__device__ unsigned long long g_ws_stamps[256 * 12 * 10];
-__device__ unsigned long long g_ws_clock[512];
-__device__ unsigned long long g_ws_tl[8192 * 2];  // per block: start, end (s_memrealtime)
-#define WS_STAMP_DECL                                \
-  unsigned long long ws_seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
-  const unsigned long long ws_t0 = __builtin_amdgcn_s_memtime(); \
-  const unsigned long long ws_r0 = __builtin_amdgcn_s_memrealtime(); \
-  if (threadIdx.x == 0 && blockIdx.x < 8192) g_ws_tl[blockIdx.x * 2] = ws_r0; \
-  unsigned long long ws_t = ws_t0
-#define WS_STAMP(k)                                              \
-  do {                                                           \
-    const unsigned long long now = __builtin_amdgcn_s_memtime(); \
-    if ((k) >= 0) ws_seg[(k) < 0 ? 0 : (k)] += now - ws_t;       \
-    ws_t = now;                                                  \
-  } while (0)
-#define WS_STAMP_SAVE                                                            \
-  do {                                                                           \
-    if (blockIdx.x < 256 && (threadIdx.x & 63) == 0)                             \
-      for (int k_ = 0; k_ < 10; ++k_)                                            \
-        g_ws_stamps[(blockIdx.x * 12 + threadIdx.x / 64) * 10 + k_] = ws_seg[k_]; \
-    if (threadIdx.x == 0 && blockIdx.x < 8192)                                   \
-      g_ws_tl[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime();            \
-    if (blockIdx.x < 256 && threadIdx.x == 0) {                                  \
-      g_ws_clock[blockIdx.x * 2] = __builtin_amdgcn_s_memtime() - ws_t0;         \
-      g_ws_clock[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime() - ws_r0; \
-    }                                                                            \
-  } while (0)
-#else
-#define WS_STAMP_DECL do {} while (0)
-#define WS_STAMP(k) do {} while (0)
-#define WS_STAMP_SAVE do {} while (0)
-#endif
-
-// LDS image: weight rows at a 160-B pitch (10 slots: the 16-lane groups of a ds_read_b128
-// read rows r and r+4.. of two units an odd number of slots apart — conflict-free), a
-// buffer of an odd number of 16-B slots (the unit pair that straddles the two buffers stays
-// odd apart), and two (bias, scale) slots for consecutive work items.
-// The tile is TH x TW pixels chosen per map at run time (TH * TW <= 512, the 8 waves' 32
-// column blocks of 16; ws_tile()): MFMA column block cb of wave wn covers tile pixels
-// q = 64 wn + 16 cb + l16 in row-major (r, c) = (q / TW, q % TW) order, so a block may wrap a
-// row.  150x300 maps take 15 x 34 tiles (90 tiles, 2% padding) instead of 16 x 32 (100
-// tiles, 14%).  The staged patch is (TH + 2) x (TW + 2) <= kWsPos positions.
-constexpr int kWsPos = 640;
+// LDS image of one buffer: NPL weight planes [64 rows][160 B] (a row = 9 taps + a zero pad
+// slot of 8 channels), then NPL input planes [(TH + 2) patch rows][PS positions][8
+// channels].  Bank rules (MI355X_MICROARCH.md §LDS; modelled lane by lane with
+// tools/lds/ws_model.py before the first run):
+//  * A fragments (ds_read_b128, lane = (row l16, unit group g)): rows at the 160-B pitch put
+//    each 16-lane group's two 8-row halves on the even slots of the bank row, offset by
+//    their units' slots; units 4s+g and 4s+g+1 are an odd number of 16-B slots apart (one
+//    tap, or the odd buffer size BUF / 16 +- 8) — conflict-free.
+//  * B fragments are read as two ds_read_b64 (32-lane groups g = 0, 1 and g = 2, 3): in the
+//    first read the even-g lanes take bytes 0-7 of their unit and the odd-g lanes bytes
+//    8-15, in the second the other halves, so the two unit groups of a 32-lane group use
+//    disjoint bank halves whatever their taps.  The odd-g lanes' fragment is then (channels
+//    4-7, 0-3), so the producers store the weight units odd-g lanes read (units 4s+g odd,
+//    i.e. tap + buffer odd) with their 8-B halves swapped.  A block of 16 pixels must then
+//    cover 16 distinct bank slots: the patch row pitch PS is TW + 16 when a block can wrap a
+//    tile row (PS = TW mod 16), TW + 2 when it cannot (TW a multiple of 16).
+//    (Round 4's single ds_read_b128 per unit conflicted 2-way in most groups: the two unit
+//    groups of a 16-lane group read taps 1 .. PW apart — 20% of the kernel's LDS cycles.)
+//  * the producers' stores are contiguous 16-B slots (ds_write_b128).
+constexpr int kWsPos = 768;     // real patch positions (TH + 2) (TW + 2): 3 per producer lane
+constexpr int kWsAlloc = 1056;  // staged positions (TH + 2) * PS, row padding included
+__host__ __device__ constexpr int ws_pitch(int tw) { return tw % 16 == 0 ? tw + 2 : tw + 16; }
 template <int WM, int WN, int MI, int NJ, int NP>
 struct WsCfg : BsCfg<WM, WN, MI, NJ, NP, false> {
   using B = BsCfg<WM, WN, MI, NJ, NP, false>;
+  // plane strides 16 B past a multiple of 512 B: the compiler would otherwise fuse two
+  // planes' ds_read_b64 into one ds_read2st64_b64 (mod-32 banks in 16-lane groups: 2x the
+  // conflicts, measured)
   static constexpr int AROW = 160;
-  static constexpr int A_PLANE = B::BM * AROW;
+  static constexpr int A_PLANE = B::BM * AROW + 16;
   static constexpr int TPIX = B::TH * B::TW;  // MFMA pixels per tile (512)
-  static constexpr int BPOS = kWsPos;
-  static constexpr int B_PLANE = BPOS * 16;
+  static constexpr int B_PLANE = kWsAlloc * 16 + 16;
   static constexpr int BUF0 = B::NPL * (A_PLANE + B_PLANE);
-  static constexpr int BUF = (BUF0 / 16) % 2 == 0 ? BUF0 + 16 : BUF0;
-  static constexpr int AUX = 2 * BUF;                 // (bias, scale) slots of two items
-  static constexpr int CTR = AUX + 4 * B::BM * 4;  // ready[2], retired[2] (TLOD_WS_FLAGS)
-  static constexpr int LDS_BYTES = CTR + 16;
+  static constexpr int BUF = (BUF0 / 16) % 2 == 0 ? BUF0 + 16 : BUF0;  // odd # of 16-B slots
+  static constexpr int AUX = 2 * BUF;  // (bias, scale) of the item
+  static constexpr int LDS_BYTES = AUX + 2 * B::BM * 4;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -882,8 +806,8 @@ __device__ __forceinline__ void bs_mac16(f32x4& acc, const V (&a)[3], const V (&
   }
 }
 
-// One work item: a whole tile (direct) or one split-K piece of a tail tile, decoded from its
-// index exactly as conv_fwd_bs_kernel decodes its block id.
+// The work item of workgroup v: a whole tile (direct) or one split-K piece of a tail tile,
+// decoded exactly as conv_fwd_bs_kernel decodes its block id.
 struct WsItem {
   int direct, split, ti, n, m0, h0, w0, c_begin, c_end;
 };
@@ -914,7 +838,7 @@ __device__ __forceinline__ WsItem ws_item(int v, int tiles_m, int tiles_w, int t
   return it;
 }
 
-template <int WM, int WN, int MI, int NJ, int NP, bool PERSIST>
+template <int WM, int WN, int MI, int NJ, int NP>
 __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     __attribute__((amdgpu_waves_per_eu(3, 3))) conv_fwd_bs_ws_kernel(
         const float* __restrict__ X, const unsigned short* __restrict__ Wp, Epi epi,
@@ -923,338 +847,149 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
   using C = WsCfg<WM, WN, MI, NJ, NP>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-  const int n_tiles = tiles_m * tiles_w * tiles_h * N;
-  const int n_tail = n_tiles - dp_tiles;
-  const int n_items = dp_tiles + (ksplit > 1 ? n_tail * ksplit : 0);
+  const int n_tail = tiles_m * tiles_w * tiles_h * N - dp_tiles;
   const int HWi = H * W;
   const int nchunks = (Cin + C::CK - 1) / C::CK;
   const int tid = threadIdx.x;
-  const int PW = TW + 2, PP = (TH + 2) * PW;  // staged patch: row pitch, positions
-  auto item = [&](int v) {
-    return ws_item(v, tiles_m, tiles_w, tiles_h, dp_tiles, n_tail, ksplit, cps, nchunks, C::BM,
-                   TH, TW);
-  };
-  // This workgroup's items are b, b + G, ...; odd workgroups take them in rotated order
-  // (last first), so that the workgroups' epilogue store bursts do not all coincide when the
-  // last item is a short split-K piece.
-  const int G = gridDim.x;
-  const int n_mine = PERSIST ? (n_items - (int)blockIdx.x + G - 1) / G : 1;
-  const int rot = TLOD_WS_ROT && (blockIdx.x & 1) ? n_mine - 1 : 0;
-  auto vidx = [&](int k) { return (int)blockIdx.x + G * ((k + rot) % n_mine); };
+  const int PW = TW + 2, PP = (TH + 2) * PW;  // real patch: row length, positions
+  const int PS = ws_pitch(TW);                 // staged row pitch (positions)
+  const WsItem it = ws_item(blockIdx.x, tiles_m, tiles_w, tiles_h, dp_tiles, n_tail, ksplit,
+                            cps, nchunks, C::BM, TH, TW);
+  const int c_begin = it.c_begin, c_end = it.c_end;
 
   if (tid >= C::NT) {
     // ================= producers: stage chunks into the two LDS buffers
-    // The producers walk the workgroup's chunk stream (item b's chunks, then item b + G's, ...)
-    // one chunk ahead in registers: every LDS store is followed by the load of the next chunk
-    // of the stream, across item boundaries.  Validity (rows past Cout, positions outside the
-    // map, channels past Cin) is applied at load time by the buffer range check (offset
-    // kBufOOB reads 0), so a chunk in registers carries no item state.  An item with an even
-    // chunk count stores the next item's first chunk into buffer 0 in its last pair's steps
-    // 3-4 (buffer 0 is retired by then), so the next item starts without a load round trip.
+    // Chunk p of the item sits in register slot p & 1 (= its LDS buffer) from its load until
+    // its store, which then loads chunk p + 2 into the slot: a chunk's loads have two
+    // chunk-steps to land.  Raw buffer loads, no element masks: rows past Cout and
+    // positions outside the map take offset kBufOOB, channels past Cin fall past the
+    // image's range — all read 0 (no 64-bit address math, no selects).
     constexpr int PT = kProdWaves * 64;
     const int ptid = tid - C::NT;
     const unsigned wrow = (unsigned)nchunks * kBsKP;  // packed row length (bf16)
     const unsigned wplane = (unsigned)Cout * wrow;    // packed plane length (bf16)
     const i32x4 w_rsrc = make_buffer_rsrc(Wp, wplane * C::NPL * 2u);
-    constexpr int A_SEG = kBsKP / 8;
+    const i32x4 x_rsrc = make_buffer_rsrc(X + (size_t)it.n * Cin * HWi, (unsigned)Cin * HWi * 4u);
+    constexpr int A_SEG = kBsKP / 8;  // 16-B segments (tap slots) per weight row
     constexpr int A_N = C::NPL * C::BM * A_SEG;
     constexpr int A_IT = (A_N + PT - 1) / PT;
-    constexpr int B_IT = (C::BPOS + PT - 1) / PT;
-    int a_lds[A_IT], a_row[A_IT];
-    unsigned a_pq[A_IT];  // plane offset + segment (elements), item-independent
+    constexpr int B_IT = (kWsPos + PT - 1) / PT;
+    // a lane's segments all have the parity of ptid (PT and the row / plane lengths are
+    // even): the segment of tap q in buffer S is stored half-swapped iff q + S is odd
+    const bool a_odd = ptid & 1;
+    int a_lds[A_IT], a_vo[A_IT];
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       const int idx = ptid + i * PT;
       const int pl = idx / (C::BM * A_SEG), rem = idx % (C::BM * A_SEG);
       const int row = rem / A_SEG, q = rem % A_SEG;
       a_lds[i] = idx < A_N ? pl * C::A_PLANE + row * C::AROW + 16 * q : -1;
-      a_row[i] = idx < A_N ? row : 1 << 30;
-      a_pq[i] = (unsigned)pl * wplane + 8u * q;
+      a_vo[i] = idx < A_N && it.m0 + row < Cout
+                    ? (int)(((unsigned)pl * wplane + 8u * q + (unsigned)(it.m0 + row) * wrow) * 2u)
+                    : kBufOOB;
     }
-    int b_pos[B_IT];
+    int b_lds[B_IT], b_vo[B_IT];
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
       const int pos = ptid + i * PT;
-      b_pos[i] = pos < PP ? C::NPL * C::A_PLANE + pos * 16 : -1;
+      const int r = pos / PW, c = pos % PW;
+      const int gh = it.h0 - 1 + r, gw = it.w0 - 1 + c;
+      b_lds[i] = pos < PP ? C::NPL * C::A_PLANE + (r * PS + c) * 16 : -1;
+      b_vo[i] = pos < PP && gh >= 0 && gh < H && gw >= 0 && gw < W ? (gh * W + gw) * 4 : kBufOOB;
     }
-    WS_STAMP_DECL;
-    // load cursor: item ld (index v_ld), chunk ch_ld
-    int k_ld = 0;
-    WsItem ld = item(vidx(0));
-    int ch_ld = ld.c_begin;
-    int a_off[A_IT], b_goff[B_IT];
-    i32x4 x_rsrc;
-    auto set_ld_item = [&]() {
+    u32x4 ra2[2][A_IT];
+    float rb2[2][B_IT][8];
+    auto load2 = [&](auto slc, int ch) {  // chunk ch -> slot S (unconditional)
+      constexpr int S = decltype(slc)::value;
+      const int cbytes = ch * C::CK * HWi * 4;
 #pragma unroll
       for (int i = 0; i < A_IT; ++i)
-        a_off[i] = ld.m0 + a_row[i] < Cout ? (int)((a_pq[i] + (unsigned)(ld.m0 + a_row[i]) * wrow) * 2u) : -1;
-#pragma unroll
-      for (int i = 0; i < B_IT; ++i) {
-        const int pos = ptid + i * PT;
-        const int r = pos / PW, c = pos % PW;
-        const int gh = ld.h0 - 1 + r, gw = ld.w0 - 1 + c;
-        b_goff[i] = pos < PP && gh >= 0 && gh < H && gw >= 0 && gw < W ? gh * W + gw : -1;
-      }
-      x_rsrc = make_buffer_rsrc(X + (size_t)ld.n * Cin * HWi, (unsigned)Cin * HWi * 4u);
-    };
-    if constexpr (!PERSIST && TLOD_WS_DEPTH2 && TLOD_WS_FLAT == 2) {
-      // One work item, two chunks in flight: chunk p of the item sits in register slot
-      // p & 1 (= its LDS buffer) from its load until its store, which then loads chunk
-      // p + 2 into the slot — a chunk's loads have two chunk-steps to land instead of one.
-      set_ld_item();
-      const int c_begin = ld.c_begin, c_end = ld.c_end;
-      // raw buffer loads, no element masks: rows past Cout and positions outside the map
-      // take offset kBufOOB, channels past Cin fall past the image's range — all read 0
-      // (fewer producer VALU than 64-bit flat addresses + selects: no 64-bit address math)
-      int a_vo[A_IT], b_vo[B_IT];
-#pragma unroll
-      for (int i = 0; i < A_IT; ++i) a_vo[i] = a_off[i] >= 0 ? a_off[i] : kBufOOB;
-#pragma unroll
-      for (int i = 0; i < B_IT; ++i) b_vo[i] = b_goff[i] >= 0 ? b_goff[i] * 4 : kBufOOB;
-      u32x4 ra2[2][A_IT];
-      float rb2[2][B_IT][8];
-      auto load2 = [&](auto slc, int ch) {  // chunk ch -> slot S (unconditional)
-        constexpr int S = decltype(slc)::value;
-        const int cbytes = ch * C::CK * HWi * 4;
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i)
-          ra2[S][i] = __builtin_bit_cast(u32x4, raw_buffer_load_v4f32(w_rsrc, a_vo[i], ch * (kBsKP * 2), 0));
-#pragma unroll
-        for (int i = 0; i < B_IT; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            rb2[S][i][e] = raw_buffer_load_f32(x_rsrc, b_vo[i], cbytes + e * HWi * 4, 0);
-      };
-      auto store2 = [&](auto slc, int ch_next) {  // slot S -> LDS buffer S; load ch_next into S
-        constexpr int S = decltype(slc)::value;
-        unsigned char* buf = smem + S * C::BUF;
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i)
-          if (a_lds[i] >= 0) *reinterpret_cast<u32x4*>(buf + a_lds[i]) = ra2[S][i];
-#pragma unroll
-        for (int i = 0; i < B_IT; ++i) {
-          if (b_pos[i] < 0) continue;
-          u32x4 sp[3];
-          float v8[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v8[e] = rb2[S][i][e];
-          split8<C::NPL>(v8, sp);
-#pragma unroll
-          for (int pl = 0; pl < C::NPL; ++pl)
-            *reinterpret_cast<u32x4*>(buf + b_pos[i] + pl * C::B_PLANE) = sp[pl];
-        }
-        // unconditional (a chunk past the item reads zeros / stale pack rows, never stored),
-        // so the compiler's vmcnt waits keep the other slot's loads in flight
-        load2(slc, ch_next);
-      };
-      const std::integral_constant<int, 0> S0;
-      const std::integral_constant<int, 1> S1;
-      load2(S0, c_begin);
-      if (c_begin + 1 < c_end) load2(S1, c_begin + 1);
-      store2(S0, c_begin + 2);                          // chunk c_begin
-      if (c_end - c_begin >= 2) store2(S1, c_begin + 3);  // chunk c_begin + 1
-      WS_STAMP(0);
-      __syncthreads();
-      WS_STAMP(8);
-      if (TLOD_WS_FLAGS) {
-        // chunks 0 and 1 are covered by the barrier (the counters start at one use each)
-        int* ready = reinterpret_cast<int*>(smem + C::CTR);
-        int* retired = ready + 2;
-        const int n = c_end - c_begin;
-        for (int j = 2; j < n; j += 2) {
-          ws_wait_ge(&retired[0], 8 * (j >> 1));  // chunk j - 2 retired from buffer 0
-          WS_STAMP(1);
-          store2(S0, c_begin + j + 2);
-          ws_signal(&ready[0]);
-          WS_STAMP(0);
-          if (j + 1 >= n) break;
-          ws_wait_ge(&retired[1], 8 * (j >> 1));
-          WS_STAMP(1);
-          store2(S1, c_begin + j + 3);
-          ws_signal(&ready[1]);
-          WS_STAMP(0);
-        }
-        WS_STAMP_SAVE;
-        return;
-      }
-      int c = c_begin;
-      // (stamp build: segment 0 = staging, k = wait at barrier Fk)
-#define WS_PSYNC(k) do { WS_STAMP(0); __syncthreads(); WS_STAMP(k); } while (0)
-      for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {  // barriers as in the loop below
-        if (c != c_begin) store2(S1, c + 3);  // chunk c+1
-        WS_PSYNC(1);
-        WS_PSYNC(2);
-        store2(S0, c + 4);  // chunk c+2
-        WS_PSYNC(3);
-        WS_PSYNC(4);
-        store2(S1, c + 5);  // chunk c+3
-        WS_PSYNC(5);
-        WS_PSYNC(6);
-        if (c + 4 < c_end) store2(S0, c + 6);  // chunk c+4
-        WS_PSYNC(7);
-      }
-#undef WS_PSYNC
-      for (; c + 1 < c_end; c += 2) {
-        if (c != c_begin) store2(S1, c + 3);  // chunk c+1
-        __syncthreads();
-        __syncthreads();
-        if (c + 2 < c_end) store2(S0, c + 4);  // chunk c+2
-        __syncthreads();
-      }
-      if ((c_end - c_begin) & 1) __syncthreads();
-      WS_STAMP(0);
-      WS_STAMP_SAVE;
-      return;
-    }
-    u32x4 ra[A_IT];
-    float rb[B_IT][8];
-    int ld_nv = 8;
-    unsigned ld_amask = ~0u, ld_bmask = ~0u;
-    auto load = [&]() {
-      const int ci0 = ch_ld * C::CK;
-      const int nv = min(C::CK, Cin - ci0);
-#if TLOD_WS_FLAT == 2
-      // unconditional loads (invalid: offset 0 / the last channel), masked right after
-      const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp) + ch_ld * (kBsKP * 2);
-#pragma unroll
-      for (int i = 0; i < A_IT; ++i) ra[i] = *reinterpret_cast<const u32x4*>(Wb + max(a_off[i], 0));
-      const float* Xc = X + (size_t)ld.n * Cin * HWi + (size_t)ci0 * HWi;
-#pragma unroll
-      for (int i = 0; i < B_IT; ++i)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) rb[i][e] = Xc[min(e, nv - 1) * HWi + max(b_goff[i], 0)];
-      ld_nv = nv;
-      ld_amask = 0;
-      ld_bmask = 0;
-#pragma unroll
-      for (int i = 0; i < A_IT; ++i) ld_amask |= (unsigned)(a_off[i] >= 0) << i;
-#pragma unroll
-      for (int i = 0; i < B_IT; ++i) ld_bmask |= (unsigned)(b_goff[i] >= 0) << i;
-#elif TLOD_WS_FLAT
-      const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wp) + ch_ld * (kBsKP * 2);
-#pragma unroll
-      for (int i = 0; i < A_IT; ++i)
-        ra[i] = *reinterpret_cast<const u32x4*>(a_off[i] >= 0 ? Wb + a_off[i]
-                                                              : reinterpret_cast<const unsigned char*>(g_zero));
-      const float* Xc = X + (size_t)ld.n * Cin * HWi + (size_t)ci0 * HWi;
+        ra2[S][i] = __builtin_bit_cast(u32x4, raw_buffer_load_v4f32(w_rsrc, a_vo[i], ch * (kBsKP * 2), 0));
 #pragma unroll
       for (int i = 0; i < B_IT; ++i)
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          rb[i][e] = *(b_goff[i] >= 0 && e < nv ? Xc + e * HWi + b_goff[i] : g_zero);
-#else
-#pragma unroll
-      for (int i = 0; i < A_IT; ++i)
-        ra[i] = __builtin_bit_cast(
-            u32x4, raw_buffer_load_v4f32(w_rsrc, a_off[i] >= 0 ? a_off[i] + ch_ld * (kBsKP * 2) : kBufOOB, 0, 0));
-#pragma unroll
-      for (int i = 0; i < B_IT; ++i)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          rb[i][e] = raw_buffer_load_f32(
-              x_rsrc, b_goff[i] >= 0 && e < nv ? ((ci0 + e) * HWi + b_goff[i]) * 4 : kBufOOB, 0, 0);
-#endif
+          rb2[S][i][e] = raw_buffer_load_f32(x_rsrc, b_vo[i], cbytes + e * HWi * 4, 0);
     };
-    auto advance = [&]() {  // the next chunk of the stream; false past its end
-      if (++ch_ld < ld.c_end) return true;
-      if (++k_ld >= n_mine) return false;
-      ld = item(vidx(k_ld));
-      ch_ld = ld.c_begin;
-      set_ld_item();
-      return true;
-    };
-    auto store = [&](unsigned char* buf) {  // registers -> buf, then load the next chunk
+    auto store2 = [&](auto slc, int ch_next) {  // slot S -> LDS buffer S; load ch_next into S
+      constexpr int S = decltype(slc)::value;
+      unsigned char* buf = smem + S * C::BUF;
+      const bool swap = a_odd != (S == 1);
 #pragma unroll
-      for (int i = 0; i < A_IT; ++i)
-        if (a_lds[i] >= 0)
-          *reinterpret_cast<u32x4*>(buf + a_lds[i]) =
-              TLOD_WS_FLAT != 2 || ((ld_amask >> i) & 1) ? ra[i] : u32x4{0, 0, 0, 0};
+      for (int i = 0; i < A_IT; ++i) {
+        const u32x4 v = ra2[S][i];
+        const u32x4 vs = swap ? u32x4{v[2], v[3], v[0], v[1]} : v;
+        if (a_lds[i] >= 0) *reinterpret_cast<u32x4*>(buf + a_lds[i]) = vs;
+      }
 #pragma unroll
       for (int i = 0; i < B_IT; ++i) {
-        if (b_pos[i] < 0) continue;
+        if (b_lds[i] < 0) continue;
         u32x4 sp[3];
         float v8[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v8[e] = TLOD_WS_FLAT != 2 || (((ld_bmask >> i) & 1) && e < ld_nv) ? rb[i][e] : 0.f;
+        for (int e = 0; e < 8; ++e) v8[e] = rb2[S][i][e];
         split8<C::NPL>(v8, sp);
 #pragma unroll
         for (int pl = 0; pl < C::NPL; ++pl)
-          *reinterpret_cast<u32x4*>(buf + b_pos[i] + pl * C::B_PLANE) = sp[pl];
+          *reinterpret_cast<u32x4*>(buf + b_lds[i] + pl * C::B_PLANE) = sp[pl];
       }
-      WS_STAMP(6);
-      if (advance()) load();
-      WS_STAMP(7);
+      // unconditional (a chunk past the item reads zeros / stale pack rows, never stored),
+      // so the compiler's vmcnt waits keep the other slot's loads in flight
+      load2(slc, ch_next);
     };
-    set_ld_item();
-    load();
-    bool prefetched = false;
-    for (int k = 0; k < n_mine; ++k) {
-      const WsItem it = item(vidx(k));
-      const int c_begin = it.c_begin, c_end = it.c_end;
-      const bool more = k + 1 < n_mine;
-      // the previous item's last barrier retired both buffers: its epilogue overlaps this
-      if (!prefetched) store(smem);                   // chunk c_begin
-      if (c_end - c_begin >= 2) store(smem + C::BUF);  // chunk c_begin + 1
-      WS_STAMP(8);
-      __syncthreads();
-      WS_STAMP(9);
-      int c = c_begin;
-      // frames of four chunks (see the MFMA waves' loop): chunks c, c + 2 in buffer 0,
-      // c + 1, c + 3 in buffer 1; seven barriers
-      for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {
-        if (c != c_begin) store(smem + C::BUF);  // chunk c+1 (buffer 1 retired at F7)
-        __syncthreads();                          // F1: c+1 visible
-        __syncthreads();                          // F2: buffer 0 (chunk c) retired
-        store(smem);                              // chunk c+2
-        __syncthreads();                          // F3: c+2 visible
-        __syncthreads();                          // F4: buffer 1 (chunk c+1) retired
-        store(smem + C::BUF);                     // chunk c+3
-        __syncthreads();                          // F5: c+3 visible
-        __syncthreads();                          // F6: buffer 0 (chunk c+2) retired
-        if (c + 4 < c_end || (c + 4 == c_end && more)) store(smem);  // chunk c+4 / next item's first
-        __syncthreads();                          // F7: buffer 1 retired, c+4 visible
-      }
-      for (; c + 1 < c_end; c += 2) {
-        WS_STAMP(-1);
-        if (c != c_begin) store(smem + C::BUF);  // chunk c+1
-        WS_STAMP(0);
-        __syncthreads();
-        WS_STAMP(1);
-        __syncthreads();
-        WS_STAMP(3);
-        if (c + 2 < c_end || (c + 2 == c_end && more)) store(smem);  // chunk c+2 / next item's first
-        WS_STAMP(4);
-        __syncthreads();
-        WS_STAMP(5);
-      }
-      prefetched = ((c_end - c_begin) & 1) == 0 && more;
-      WS_STAMP(-1);
-      if ((c_end - c_begin) & 1) __syncthreads();  // the lone last chunk retires buffer 0
+    const std::integral_constant<int, 0> S0;
+    const std::integral_constant<int, 1> S1;
+    load2(S0, c_begin);
+    if (c_begin + 1 < c_end) load2(S1, c_begin + 1);
+    store2(S0, c_begin + 2);                            // chunk c_begin
+    if (c_end - c_begin >= 2) store2(S1, c_begin + 3);  // chunk c_begin + 1
+    __syncthreads();
+    int c = c_begin;
+    for (; c + 3 < c_end; c += 4) {  // barriers F1..F7 as in the MFMA waves' frame
+      if (c != c_begin) store2(S1, c + 3);  // chunk c+1 (buffer 1 retired at F7)
+      __syncthreads();                      // F1: c+1 visible
+      __syncthreads();                      // F2: buffer 0 (chunk c) retired
+      store2(S0, c + 4);                    // chunk c+2
+      __syncthreads();                      // F3: c+2 visible
+      __syncthreads();                      // F4: buffer 1 (chunk c+1) retired
+      store2(S1, c + 5);                    // chunk c+3
+      __syncthreads();                      // F5: c+3 visible
+      __syncthreads();                      // F6: buffer 0 (chunk c+2) retired
+      if (c + 4 < c_end) store2(S0, c + 6);  // chunk c+4
+      __syncthreads();                      // F7: buffer 1 retired, c+4 visible
     }
-    WS_STAMP_SAVE;
+    for (; c + 1 < c_end; c += 2) {
+      if (c != c_begin) store2(S1, c + 3);  // chunk c+1
+      __syncthreads();
+      __syncthreads();
+      if (c + 2 < c_end) store2(S0, c + 4);  // chunk c+2
+      __syncthreads();
+    }
+    if ((c_end - c_begin) & 1) __syncthreads();  // the lone last chunk retires buffer 0
     return;
   }
 
   // ================= MFMA waves
   // The wave's 64 x 64 output block is 4 x 4 tiles of 16 x 16 (row block rb = 16 output
-  // channels; column block cb = (pixel row j, half hh) = 16 pixels).  One k-step takes four
-  // (tap, 8-channel) units, lane group g = lane / 16 reading unit 4s + g; the 16x16x16 step
-  // takes units 16, 17 (lanes 0-31 / 32-63, 8-B halves by (lane / 16) & 1).
+  // channels; column block cb = 16 pixels).  One k-step takes four (tap, 8-channel) units,
+  // lane group g = lane / 16 reading unit 4s + g; the 16x16x16 step takes units 16, 17
+  // (lanes 0-31 / 32-63, 8-B halves by (lane / 16) & 1).
   const int lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int l16 = lane & 15, g = lane >> 4;
   constexpr int RB = MI * 2, CB = NJ * 2;
   const int a_lane = (wm * MI * 32 + l16) * C::AROW;
-  auto tap_c = [&](int tap) { return ((tap / 3) * PW + tap % 3) * 16; };
-  // column block cb: this lane's pixel q = 64 wn + 16 cb + l16 of the tile, at patch
-  // position (q / TW) * PW + q % TW for tap (0, 0); pixels past the tile read position 0
-  // (their results are never stored)
+  auto tap_c = [&](int tap) { return ((tap / 3) * PS + tap % 3) * 16; };
+  // column block cb: this lane's pixel q = 64 wn + 16 cb + l16 of the tile in row-major (r,
+  // c) = (q / TW, q % TW) order (a block may wrap a tile row), at staged position r PS + c
+  // for tap (0, 0), plus the lane's first-read half (8 B for odd g); pixels past the tile
+  // read a pixel of the tile (their results are never stored)
+  const int hb = 8 * (g & 1);
   int bpix[CB];
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
-    const int q = wn * 64 + cb * 16 + l16;
-    bpix[cb] = C::NPL * C::A_PLANE + (q < TH * TW ? (q / TW) * PW + q % TW : 0) * 16;
+    const int q = (wn * 64 + cb * 16 + l16) % (TH * TW);
+    bpix[cb] = C::NPL * C::A_PLANE + ((q / TW) * PS + q % TW) * 16 + hb;
   }
   // (the asm keeps the compiler from hoisting all 20 (unit, block) sums out of the loop
   // into registers)
@@ -1278,19 +1013,15 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
     asm volatile("" : "+v"(gg));
     return ub((4 * s + gg) % 18);
   };
-  const int hb = 8 * (g & 1);
-  const int aoff4 = a_lane + ua(16 + (lane >> 5)) + hb;
-  const int boff4 = ub(16 + (lane >> 5)) + hb;
-  // lone last chunk: (8, pad) — slot 9 of a weight row is zero
-  const int aoffL = a_lane + 16 * (8 + (lane >> 5)) + hb, boffL = tap_c(8) + hb;
+  // 16x16x16 step of a pair: lanes 0-31 unit 16 (unswapped), 32-63 unit 17 (stored
+  // half-swapped: the A half is the other one)
+  const int aoff4 = a_lane + ua(16 + (lane >> 5)) + ((lane >> 5) ? 8 - hb : hb);
+  const int boff4 = ub(16 + (lane >> 5));
+  // lone last chunk: (8, pad) — slot 9 of a weight row is zero; tap 8 of buffer 0 unswapped
+  const int aoffL = a_lane + 16 * (8 + (lane >> 5)) + hb, boffL = tap_c(8);
 
   f32x4 acc[RB][CB];
-  // TLOD_WS_PRIO: 1 = the younger half of the MFMA waves (4-7) at priority 1 for the whole
-  // kernel; 2 = priority 1 around every k-step's MFMA cluster (cdna_hip_programming.md T5)
-  if (TLOD_WS_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
-    __builtin_amdgcn_s_setprio(1);
   auto step16 = [&](int ao, int bo) {
-    if (TLOD_WS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     u32x4 a[RB][3];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -1299,14 +1030,17 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
         a[rb][pl] = *reinterpret_cast<const u32x4*>(smem + ao + pl * C::A_PLANE + rb * 16 * C::AROW);
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) {
+      const int b0 = baddr(cb, bo), b1 = b0 ^ 8;  // this lane's two 8-B halves, in order
       u32x4 b[3];
 #pragma unroll
-      for (int pl = 0; pl < C::NPL; ++pl)
-        b[pl] = *reinterpret_cast<const u32x4*>(smem + baddr(cb, bo) + pl * C::B_PLANE);
+      for (int pl = 0; pl < C::NPL; ++pl) {
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(smem + b0 + pl * C::B_PLANE);
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(smem + b1 + pl * C::B_PLANE);
+        b[pl] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) bs_mac16<NP>(acc[rb][cb], a[rb], b, mfma16_bf16);
     }
-    if (TLOD_WS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   };
   auto step8 = [&](int ao, int bo) {
     u32x2 a[RB][3];
@@ -1328,240 +1062,160 @@ __global__ void __launch_bounds__(WM* WN * 64 + kProdWaves * 64)
 
   constexpr int TP = C::TPIX;
   const bool has_scale = epi.scale != nullptr;
-  WS_STAMP_DECL;
-  int k = 0;
-  for (; k < n_mine; ++k) {
-    const WsItem it = item(vidx(k));
-    float* bias_s = reinterpret_cast<float*>(smem + C::AUX) + (k & 1) * 2 * C::BM;
-    float* scale_s = bias_s + C::BM;
-    if (tid < C::BM) {
-      const int co = min(it.m0 + tid, Cout - 1);
-      bias_s[tid] = epi.bias ? epi.bias[co] : 0.f;
-      scale_s[tid] = epi.scale ? epi.scale[co] : 1.f;
-    }
-    int* ready = reinterpret_cast<int*>(smem + C::CTR);
-    int* retired = ready + 2;
-    if (!PERSIST && TLOD_WS_FLAGS && tid < 4) ready[tid] = tid < 2 ? 4 : 0;
+  float* bias_s = reinterpret_cast<float*>(smem + C::AUX);
+  float* scale_s = bias_s + C::BM;
+  if (tid < C::BM) {
+    const int co = min(it.m0 + tid, Cout - 1);
+    bias_s[tid] = epi.bias ? epi.bias[co] : 0.f;
+    scale_s[tid] = epi.scale ? epi.scale[co] : 1.f;
+  }
 #pragma unroll
-    for (int i = 0; i < RB; ++i)
+  for (int i = 0; i < RB; ++i)
 #pragma unroll
-      for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    WS_STAMP(0);
+    for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  int c = c_begin;
+  // Four chunks (36 (tap, 8-channel) units) are nine 16x16x32 k-steps; a chunk pair's 18
+  // units leave a 16x16x16 step, which issues at the 16x16x32's 16 cycles for half the
+  // work (tools/probe/mfma_rate.hip), so whole frames run first.  Steps 2, 4 and 6 read
+  // two chunks (both buffers); a buffer is refilled once its chunk's last step is done.
+  for (; c + 3 < c_end; c += 4) {
+    step16(aoff_s(0), boff_s(0));
+    step16(aoff_s(1), boff_s(1));
+    __syncthreads();  // F1
+    step16(aoff_s(2), boff_s(2));
+    __syncthreads();  // F2
+    step16(aoff_s(3), boff_s(3));
+    __syncthreads();  // F3
+    step16(aoff_s(4), boff_s(4));
+    __syncthreads();  // F4
+    step16(aoff_s(5), boff_s(5));
+    __syncthreads();  // F5
+    step16(aoff_s(6), boff_s(6));
+    __syncthreads();  // F6
+    step16(aoff_s(7), boff_s(7));
+    step16(aoff_s(8), boff_s(8));
+    __syncthreads();  // F7
+  }
+  for (; c + 1 < c_end; c += 2) {
+    step16(aoff_s(0), boff_s(0));
+    step16(aoff_s(1), boff_s(1));
+    __syncthreads();  // chunk c+1 visible
+    step16(aoff_s(2), boff_s(2));
+    __syncthreads();  // buffer 0 retired
+    step16(aoff_s(3), boff_s(3));
+    step8(aoff4, boff4);
     __syncthreads();
-    WS_STAMP(8);
-    int c = it.c_begin;
-    const int c_end = it.c_end;
-    if constexpr (!PERSIST && TLOD_WS_FLAGS) {
-      // relative chunk j lives in buffer j & 1 as its (j >> 1)-th use: ready when the
-      // buffer's count reaches 4 ((j >> 1) + 1) (four producer waves), retired by the eight
-      // MFMA waves' adds
-      auto wait_ready = [&](int j) {
-        WS_STAMP(0);
-        ws_wait_ge(&ready[j & 1], 4 * ((j >> 1) + 1));
-        WS_STAMP(1);
-      };
-      auto retire = [&](int j) { ws_signal(&retired[j & 1]); };
-      int j = 0;
-      for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4, j += 4) {
-        wait_ready(j);
-        step16(aoff_s(0), boff_s(0));
-        step16(aoff_s(1), boff_s(1));
-        wait_ready(j + 1);
-        step16(aoff_s(2), boff_s(2));
-        retire(j);
-        step16(aoff_s(3), boff_s(3));
-        wait_ready(j + 2);
-        step16(aoff_s(4), boff_s(4));
-        retire(j + 1);
-        step16(aoff_s(5), boff_s(5));
-        wait_ready(j + 3);
-        step16(aoff_s(6), boff_s(6));
-        retire(j + 2);
-        step16(aoff_s(7), boff_s(7));
-        step16(aoff_s(8), boff_s(8));
-        retire(j + 3);
-      }
-      for (; c + 1 < c_end; c += 2, j += 2) {
-        wait_ready(j);
-        step16(aoff_s(0), boff_s(0));
-        step16(aoff_s(1), boff_s(1));
-        wait_ready(j + 1);
-        step16(aoff_s(2), boff_s(2));
-        retire(j);
-        step16(aoff_s(3), boff_s(3));
-        step8(aoff4, boff4);
-        retire(j + 1);
-      }
-      if (c < c_end) {
-        wait_ready(j);
-        step16(aoff_s(0), boff_s(0));
-        step16(aoff_s(1), boff_s(1));
-        step8(aoffL, boffL);
-      }
-      c = c_end;
-    }
-    // Four chunks (36 (tap, 8-channel) units) are nine 16x16x32 k-steps; a chunk pair's 18
-    // units leave a 16x16x16 step, which issues at the 16x16x32's 16 cycles for half the
-    // work (tools/probe/mfma_rate.hip), so whole frames run first.  Steps 2, 4 and 6 read
-    // two chunks (both buffers); a buffer is refilled once its chunk's last step is done.
-    // (stamp build: segment 0 = k-steps, 1 = barrier waits)
-#define WS_SYNC(k) do { WS_STAMP(0); __syncthreads(); WS_STAMP(k); } while (0)
-    for (; TLOD_WS_FRAME && c + 3 < c_end; c += 4) {
-      step16(aoff_s(0), boff_s(0));
-      step16(aoff_s(1), boff_s(1));
-      WS_SYNC(1);  // F1
-      step16(aoff_s(2), boff_s(2));
-      WS_SYNC(2);  // F2
-      step16(aoff_s(3), boff_s(3));
-      WS_SYNC(3);  // F3
-      step16(aoff_s(4), boff_s(4));
-      WS_SYNC(4);  // F4
-      step16(aoff_s(5), boff_s(5));
-      WS_SYNC(5);  // F5
-      step16(aoff_s(6), boff_s(6));
-      WS_SYNC(6);  // F6
-      step16(aoff_s(7), boff_s(7));
-      step16(aoff_s(8), boff_s(8));
-      WS_SYNC(7);  // F7
-    }
-#undef WS_SYNC
-    for (; c + 1 < c_end; c += 2) {
-      WS_STAMP(-1);
-      step16(aoff_s(0), boff_s(0));
-      step16(aoff_s(1), boff_s(1));
-      WS_STAMP(0);
-      __syncthreads();  // chunk c+1 visible
-      WS_STAMP(1);
-      step16(aoff_s(2), boff_s(2));
-      WS_STAMP(2);
-      __syncthreads();  // buffer 0 retired
-      WS_STAMP(3);
-      step16(aoff_s(3), boff_s(3));
-      step8(aoff4, boff4);
-      WS_STAMP(4);
-      __syncthreads();
-      WS_STAMP(5);
-    }
-    if (c < c_end) {
-      step16(aoff_s(0), boff_s(0));
-      step16(aoff_s(1), boff_s(1));
-      step8(aoffL, boffL);
-      __syncthreads();
-    }
-    WS_STAMP(0);
+  }
+  if (c < c_end) {
+    step16(aoff_s(0), boff_s(0));
+    step16(aoff_s(1), boff_s(1));
+    step8(aoffL, boffL);
+    __syncthreads();
+  }
 
-    // epilogue: the lane holds rows 4g..4g+3 of column l16 of each 16 x 16 tile
-    if (!it.direct) {
-      float* St = slab + ((size_t)it.split * n_tail + it.ti) * C::BM * TP;
+  // epilogue: the lane holds rows 4g..4g+3 of column l16 of each 16 x 16 tile
+  if (!it.direct) {
+    float* St = slab + ((size_t)it.split * n_tail + it.ti) * C::BM * TP;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
-            St[ml * TP + wn * 64 + cb * 16 + l16] = acc[rb][cb][r];
-          }
-      WS_STAMP(7);
-      continue;
-    }
-    bool pooled = false;
-    if constexpr (NJ == 2) {
-      if (epi.pool) {
-        // max_pool2d(2, 2) window (16 x 32 tiles only, see ws_tile): pixel rows j = 0, 1
-        // (column blocks hh and 2 + hh), columns (l16, l16 ^ 1); torch's window order and
-        // update rule, as conv_fwd_bs_kernel
-        pooled = true;
-        const int Hp = H / 2, Wp2 = W / 2;
-        float* Pn = epi.pool + (size_t)it.n * Cout * Hp * Wp2;
-        const int hp = (it.h0 + wn * NJ) / 2;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int wp = (it.w0 + hh * 16 + l16) / 2;
-          const bool writer = (l16 & 1) == 0 && hp < Hp && wp < Wp2;
-#pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
-              float v2[2];
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                v2[j] = acc[rb][j * 2 + hh][r];
-                if (has_scale) v2[j] *= scale_s[ml];
-                v2[j] += bias_s[ml];
-                if (epi.relu) v2[j] = fmaxf(v2[j], 0.f);
-              }
-              const float c0 = __shfl_xor(v2[0], 1), c1 = __shfl_xor(v2[1], 1);
-              float m = v2[0];
-              if (c0 > m || __builtin_isnan(c0)) m = c0;
-              if (v2[1] > m || __builtin_isnan(v2[1])) m = v2[1];
-              if (c1 > m || __builtin_isnan(c1)) m = c1;
-              if (writer && it.m0 + ml < Cout) Pn[((size_t)(it.m0 + ml) * Hp + hp) * Wp2 + wp] = m;
-            }
-        }
-      }
-    }
-    if (!pooled) {
-      // Branch-free: 32-bit offsets into the image's planes through buffer resources; an
-      // element outside the tile / map / Cout gets offset kBufOOB, which the hardware drops
-      // (store) or reads as 0 (residual / mask load).  The per-element bounds checks and
-      // 64-bit addresses of a plain store epilogue compiled to ~10 branchy instructions per
-      // element: 29k of a tile's 317k cycles with the stores themselves removed (round 4).
-      const size_t img_off = (size_t)it.n * Cout * HWi;
-      const unsigned plane_bytes = (unsigned)Cout * HWi * 4u;
-      const i32x4 y_rsrc = make_buffer_rsrc(Y + img_off, plane_bytes);
-      const float* Rn = epi.residual ? epi.residual + img_off : nullptr;
-      const float* Mn = epi.mask ? epi.mask + img_off : nullptr;
-      const i32x4 r_rsrc = make_buffer_rsrc(Rn ? Rn : Y, Rn ? plane_bytes : 0u);
-      const i32x4 m_rsrc = make_buffer_rsrc(Mn ? Mn : Y, Mn ? plane_bytes : 0u);
-      int pixo[CB];  // byte offset of the lane's pixel in a channel plane (-1: none)
-#pragma unroll
-      for (int cb = 0; cb < CB; ++cb) {
-        const int q = wn * 64 + cb * 16 + l16;
-        const int h = it.h0 + q / TW, w = it.w0 + q % TW;
-        pixo[cb] = q < TH * TW && h < H && w < W ? (h * W + w) * 4 : -1;
-      }
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        int off[CB][4];
+      for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
-          const int rowo = co < Cout ? co * HWi * 4 : -1;
-#pragma unroll
-          for (int cb = 0; cb < CB; ++cb) off[cb][r] = (rowo | pixo[cb]) >= 0 ? rowo + pixo[cb] : kBufOOB;
+          const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
+          St[ml * TP + wn * 64 + cb * 16 + l16] = acc[rb][cb][r];
         }
-        // residual / mask operands of the row block loaded together, ahead of its stores
-        float ext[CB][4], msk[CB][4];
+    return;
+  }
+  if constexpr (NJ == 2) {
+    if (epi.pool) {
+      // max_pool2d(2, 2) window (16 x 32 tiles only, see ws_tile): pixel rows j = 0, 1
+      // (column blocks hh and 2 + hh), columns (l16, l16 ^ 1); torch's window order and
+      // update rule, as conv_fwd_bs_kernel
+      const int Hp = H / 2, Wp2 = W / 2;
+      float* Pn = epi.pool + (size_t)it.n * Cout * Hp * Wp2;
+      const int hp = (it.h0 + wn * NJ) / 2;
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
+      for (int hh = 0; hh < 2; ++hh) {
+        const int wp = (it.w0 + hh * 16 + l16) / 2;
+        const bool writer = (l16 & 1) == 0 && hp < Hp && wp < Wp2;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            ext[cb][r] = Rn ? raw_buffer_load_f32(r_rsrc, off[cb][r], 0, 0) : 0.f;
-            msk[cb][r] = Mn ? raw_buffer_load_f32(m_rsrc, off[cb][r], 0, 0) : 1.f;
-          }
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
+        for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
-            float val = acc[rb][cb][r];
-            if (has_scale) val *= scale_s[ml];
-            val += bias_s[ml];
-            if (Rn) val += ext[cb][r];
-            if (epi.relu) val = fmaxf(val, 0.f);
-            if (Mn && !(msk[cb][r] > 0.f)) val = 0.f;
-#if TLOD_WS_NOSTORE  // timing-only diagnostic build: the epilogue's stores dropped
-            off[cb][r] = kBufOOB;
-#endif
-            raw_buffer_store_f32(val, y_rsrc, off[cb][r], 0, 0);
+            float v2[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              v2[j] = acc[rb][j * 2 + hh][r];
+              if (has_scale) v2[j] *= scale_s[ml];
+              v2[j] += bias_s[ml];
+              if (epi.relu) v2[j] = fmaxf(v2[j], 0.f);
+            }
+            const float c0 = __shfl_xor(v2[0], 1), c1 = __shfl_xor(v2[1], 1);
+            float m = v2[0];
+            if (c0 > m || __builtin_isnan(c0)) m = c0;
+            if (v2[1] > m || __builtin_isnan(v2[1])) m = v2[1];
+            if (c1 > m || __builtin_isnan(c1)) m = c1;
+            if (writer && it.m0 + ml < Cout) Pn[((size_t)(it.m0 + ml) * Hp + hp) * Wp2 + wp] = m;
           }
       }
+      return;
     }
-    WS_STAMP(9);
   }
-  WS_STAMP_SAVE;
+  // Branch-free: 32-bit offsets into the image's planes through buffer resources; an
+  // element outside the tile / map / Cout gets offset kBufOOB, which the hardware drops
+  // (store) or reads as 0 (residual / mask load).  The per-element bounds checks and 64-bit
+  // addresses of a plain store epilogue compiled to ~10 branchy instructions per element:
+  // 29k of a tile's 317k cycles with the stores themselves removed (round 4).
+  const size_t img_off = (size_t)it.n * Cout * HWi;
+  const unsigned plane_bytes = (unsigned)Cout * HWi * 4u;
+  const i32x4 y_rsrc = make_buffer_rsrc(Y + img_off, plane_bytes);
+  const float* Rn = epi.residual ? epi.residual + img_off : nullptr;
+  const float* Mn = epi.mask ? epi.mask + img_off : nullptr;
+  const i32x4 r_rsrc = make_buffer_rsrc(Rn ? Rn : Y, Rn ? plane_bytes : 0u);
+  const i32x4 m_rsrc = make_buffer_rsrc(Mn ? Mn : Y, Mn ? plane_bytes : 0u);
+  int pixo[CB];  // byte offset of the lane's pixel in a channel plane (-1: none)
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    const int q = wn * 64 + cb * 16 + l16;
+    const int h = it.h0 + q / TW, w = it.w0 + q % TW;
+    pixo[cb] = q < TH * TW && h < H && w < W ? (h * W + w) * 4 : -1;
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    int off[CB][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = it.m0 + wm * MI * 32 + rb * 16 + 4 * g + r;
+      const int rowo = co < Cout ? co * HWi * 4 : -1;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) off[cb][r] = (rowo | pixo[cb]) >= 0 ? rowo + pixo[cb] : kBufOOB;
+    }
+    // residual / mask operands of the row block loaded together, ahead of its stores
+    float ext[CB][4], msk[CB][4];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ext[cb][r] = Rn ? raw_buffer_load_f32(r_rsrc, off[cb][r], 0, 0) : 0.f;
+        msk[cb][r] = Mn ? raw_buffer_load_f32(m_rsrc, off[cb][r], 0, 0) : 1.f;
+      }
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ml = wm * MI * 32 + rb * 16 + 4 * g + r;
+        float val = acc[rb][cb][r];
+        if (has_scale) val *= scale_s[ml];
+        val += bias_s[ml];
+        if (Rn) val += ext[cb][r];
+        if (epi.relu) val = fmaxf(val, 0.f);
+        if (Mn && !(msk[cb][r] > 0.f)) val = 0.f;
+        raw_buffer_store_f32(val, y_rsrc, off[cb][r], 0, 0);
+      }
+  }
 }
 
 // Packed, pre-split weights for conv_fwd_bs_kernel: three bf16 planes (hi, mid, lo of the
@@ -2430,8 +2084,7 @@ static bool use_band(int H, int W) {
 // Warp-specialized forward for 2D tiles with >= 16 input-channel chunks (Cin >= 128):
 // measured 5-8% faster on conv3/conv4 fwd and dgrad, ~2% slower at Cin = 64 (4 chunk pairs
 // per tile: the per-tile prologue dominates).  TLOD_CONV_WS=0 disables it.
-// One predicate for the plan (resident slots) and the launch.  Only the raw-buffer-load
-// build (TLOD_WS_FLAT == 0) has 32-bit offsets into one image.
+// One predicate for the plan (resident slots) and the launch.
 static bool use_ws(int Cin, int Cout, int H, int W) {
   static const bool ws = tune_knob("TLOD_CONV_WS", 1) != 0;
   static const int min_cin = tune_knob("TLOD_WS_MINCIN", 128);
@@ -2440,9 +2093,10 @@ static bool use_ws(int Cin, int Cout, int H, int W) {
 }
 
 // Tile of the warp-specialized kernel for an H x W map: the fewest tiles of TH x TW <= 512
-// pixels whose (TH + 2) x (TW + 2) patch fits kWsPos positions; ties go to the smaller halo
-// (patch / pixels, to 0.05), then the wider tile (coalesced staging rows).  Pooling epilogues
-// and TLOD_WS_FLEX=0 keep 16 x 32.
+// pixels whose patch fits the staging (real (TH + 2) x (TW + 2) <= kWsPos positions, staged
+// (TH + 2) x ws_pitch(TW) <= kWsAlloc); ties go to the smaller halo (patch / pixels, to
+// 0.05), then the wider tile (coalesced staging rows).  Pooling epilogues and
+// TLOD_WS_FLEX=0 keep 16 x 32.
 struct WsTile {
   int th, tw;
 };
@@ -2452,23 +2106,23 @@ static WsTile ws_tile(int H, int W, bool pool) {
   WsTile best{16, 32};
   long long best_t = (long long)div_up(H, 16) * div_up(W, 32);
   int best_h = 24;  // halo of 16 x 32 (612 / 512 = 1.195) in units of 0.05
-  for (int th = 1; th <= std::min(H, 64); ++th) {
-    const int tw = std::min({512 / th, kWsPos / (th + 2) - 2, W});
-    if (tw < 8) continue;
-    const long long t = (long long)div_up(H, th) * div_up(W, tw);
-    const int halo = (int)std::lround(20.0 * (th + 2) * (tw + 2) / (th * tw));
-    if (t < best_t || (t == best_t && (halo < best_h || (halo == best_h && tw > best.tw)))) {
-      best = {th, tw};
-      best_t = t;
-      best_h = halo;
+  for (int th = 1; th <= std::min(H, 64); ++th)
+    for (int tw = 8; tw <= std::min(512 / th, W); ++tw) {
+      if ((th + 2) * (tw + 2) > kWsPos || (th + 2) * ws_pitch(tw) > kWsAlloc) continue;
+      const long long t = (long long)div_up(H, th) * div_up(W, tw);
+      const int halo = (int)std::lround(20.0 * (th + 2) * (tw + 2) / (th * tw));
+      if (t < best_t || (t == best_t && (halo < best_h || (halo == best_h && tw > best.tw)))) {
+        best = {th, tw};
+        best_t = t;
+        best_h = halo;
+      }
     }
-  }
   return best;
 }
 
 template <int WM, int WN, int MI, int NJ, int NP>
 static int ws_slots() {
-  static const int slots = resident_slots(conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP, true>,
+  static const int slots = resident_slots(conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>,
                                           WM * WN * 64 + kProdWaves * 64,
                                           WsCfg<WM, WN, MI, NJ, NP>::LDS_BYTES);
   return slots;
@@ -2496,7 +2150,7 @@ static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_sp
   FwdPlan p = plan_schedule(div_up(Cout, C::BM), tw, th, N, nchunks,
                             2.0 * C::BM * C::TH * C::TW * (double)nchunks * 72 * NP / 16.0,
                             C::BM * C::TH * C::TW, slots, allow_split,
-                            ws && TLOD_WS_FRAME && nchunks >= 16 ? 4 : 1);
+                            ws && nchunks >= 16 ? 4 : 1);
   if (ws) {
     p.th = wt.th;
     p.tw = wt.tw;
@@ -2518,22 +2172,17 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
   }
   bool launched = false;
   if constexpr (!BAND) {
-    // warp-specialized kernel (persistent: at most one workgroup per slot)
+    // warp-specialized kernel: one work item per workgroup
     if (use_ws(Cin, Cout, H, W)) {
       using WC = WsCfg<WM, WN, MI, NJ, NP>;
-      // persistent (TLOD_WS_PERSIST=1) or one work item per workgroup (default: measured
-      // faster — an exiting workgroup's output stores drain while the next one stages)
-      static const bool persist = tune_knob("TLOD_WS_PERSIST", 0) != 0;
-      auto kern = persist ? conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP, true>
-                          : conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP, false>;
+      auto kern = conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>;
       static bool attr = false;
       if (!attr) {
         TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)WC::LDS_BYTES));
         attr = true;
       }
-      const long long grid = persist ? std::min<long long>(nwg, ws_slots<WM, WN, MI, NJ, NP>()) : nwg;
-      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C::NT + kProdWaves * 64), WC::LDS_BYTES,
+      hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT + kProdWaves * 64), WC::LDS_BYTES,
                          s, X, Wp, epi, Y, N, Cin, H, W, Cout, p.tiles_m, p.tiles_w, p.tiles_h,
                          p.dp_tiles, p.ksplit, p.cps, slab, p.th, p.tw);
       launched = true;
@@ -2751,18 +2400,6 @@ static int with_wgrad_bs_cfg(int N, int Cin, int H, int W, int Cout, int KS, int
 
 using namespace tlod;
 
-#if TLOD_WS_STAMPS
-extern "C" int tlod_debug_ws_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_stamps), sizeof(g_ws_stamps)) == hipSuccess &&
-                 hipMemcpyFromSymbol(host + 256 * 12 * 10, HIP_SYMBOL(g_ws_clock),
-                                     sizeof(g_ws_clock)) == hipSuccess
-             ? 0
-             : 1;
-}
-extern "C" int tlod_debug_ws_timeline(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_tl), sizeof(g_ws_tl)) == hipSuccess ? 0 : 1;
-}
-#endif
 
 extern "C" int tlod_conv_pack_fwd_f32(const float* weight, int Cout, int Cin, int KS, float* wk,
                                       tlod_stream_t stream) {
