@@ -18,13 +18,11 @@
  *   TLOD_ROI_BWD_GATHER=0  RoIAlignAvg backward on the atomic kernels instead of the
  *                          deterministic sorted-tap gather (the gather workspace query then
  *                          returns 0);
- *   TLOD_ROI_BWD_LDS=1     with the gather off: the LDS-accumulation backward kernel;
  *   TLOD_WGRAD_WS=0        3x3 bf16x6 weight gradient on the im2col kernel instead of the
  *                          warp-specialized pixel-tile kernel;
  *   TLOD_WG1X1_TILE=256|128  1x1 split-bf16 weight gradient tile (default: cost model);
- *   TLOD_GEMM_WS=1         bf16x6 GEMMs on the warp-specialized kernel (csrc/gemm_ws.hip);
  *   TLOD_CONV_KSPLIT_MAX=n, TLOD_WGWS_SPLIT_MAX=n  caps on the split-K planners (A/B only);
- *   TLOD_CONV_WS=0, TLOD_WS_MINCIN=n, TLOD_WS_FLEX=0, TLOD_WS_PERSIST=1, TLOD_CONV_BAND=0,
+ *   TLOD_CONV_WS=0, TLOD_WS_MINCIN=n, TLOD_WS_FLEX=0, TLOD_CONV_BAND=0,
  *   TLOD_CONV_FWD_CK=4, TLOD_CONV_WGRAD_TH=2
  *                          split-bf16 / f32 conv forward tilings (see csrc/conv.hip);
  * the workspace queries follow the same switches, so query after setting them.
@@ -321,8 +319,7 @@ int tlod_conv_dgrad_bs_mask_f32(const float* dy, const void* wp, const float* ma
  * A(m,k) = a[m*K + k] if a_kcontig else a[k*M + m];  B(n,k) = b[n*K + k] if b_kcontig else
  * b[k*N + n].  Operands split exactly into bf16 planes, nprod (6 or 3) products per f32
  * product on the bf16 MFMA, f32 accumulation; split-K through a caller workspace of
- * tlod_gemm_bs_workspace_bytes (fixed-order reduction: deterministic).  TLOD_GEMM_WS=1 runs
- * nprod = 6 on the warp-specialized kernel (csrc/gemm_ws.hip, opt-in: slower on the head). */
+ * tlod_gemm_bs_workspace_bytes (fixed-order reduction: deterministic). */
 size_t tlod_gemm_bs_workspace_bytes(int M, int N, int K, int a_kcontig, int b_kcontig, int nprod);
 int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c, int M, int N,
                      int K, int a_kcontig, int b_kcontig, int nprod, void* ws, size_t ws_bytes,

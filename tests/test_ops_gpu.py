@@ -90,8 +90,7 @@ def test_roi_align_fwd_bwd(B, C, H, W, R, ah, aw):
 def test_roi_align_avg_fused(B, C, H, W, R, path, monkeypatch):
     """Odd C, RoIs of two images interleaved; (2, 33, 37, 75, 556) is the DAF step's RoI
     count on its base-feature map; backward through the default sorted-tap gather and the
-    atomic kernels (TLOD_ROI_BWD_GATHER=0; the opt-in LDS-accumulation backward,
-    TLOD_ROI_BWD_LDS=1, passed these cases too)."""
+    atomic kernels (TLOD_ROI_BWD_GATHER=0)."""
     from tlod.roi_align import RoIAlignAvg
     monkeypatch.setenv("TLOD_ROI_BWD_GATHER", "1" if path == "gather" else "0")
     rng = np.random.default_rng(R)

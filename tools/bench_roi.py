@@ -1,7 +1,6 @@
 """Microbenchmark: RoIAlignAvg 7x7 backward on the DAF step's shape (2 images, base feature
 512 x 37 x 75, 256 source + 300 target RoIs of realistic sizes): the sorted-tap gather
-(default, no atomics), TLOD_ROI_BWD_GATHER=0 the global-atomic NHWC kernel,
-TLOD_ROI_BWD_GATHER=0 TLOD_ROI_BWD_LDS=1 the LDS-accumulation kernel."""
+(default, no atomics), TLOD_ROI_BWD_GATHER=0 the global-atomic NHWC kernel."""
 import json
 import os
 import sys
@@ -49,9 +48,7 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / 20 * 1e3
-    kind = ("atomic" if os.environ.get("TLOD_ROI_BWD_GATHER") == "0" and
-            os.environ.get("TLOD_ROI_BWD_LDS") != "1" else
-            "lds" if os.environ.get("TLOD_ROI_BWD_GATHER") == "0" else "gather")
+    kind = "atomic" if os.environ.get("TLOD_ROI_BWD_GATHER") == "0" else "gather"
     print(json.dumps({"kernel": kind, "roi_align_avg_bwd_us": round(us, 1),
                       "R": R, "C": C, "map": [H, W]}))
 

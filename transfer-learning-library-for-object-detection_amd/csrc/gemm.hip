@@ -15,7 +15,8 @@
 // nprod = 6 (or 3) bf16 products per f32 product on v_mfma_f32_32x32x16_bf16, f32
 // accumulation — the same f32-level error as the conv kernels (tests/test_linear_gpu.py).
 // Tiles 256 x 256 x 16 (8 waves, 4x2 accumulators of 32x32 each), LDS double-buffered.
-// K-contiguous operands are staged [row][16 k] (pitch 48 B, ds_read_b128 conflict-free);
+// K-contiguous operands are staged [row][16 k] (32-B rows, the 16-B halves swapped on rows
+// with bit 3 set: conflict-free for the staging ds_write_b64 and the fragment reads);
 // M/N-contiguous ones [16 k][256] (pitch 576 B) and read with the gfx950 transposing
 // ds_read_b64_tr_b16, so every global load is a coalesced buffer_load_dwordx4 whatever the
 // layout.  Rows/columns past M/N read out of the buffer range (zero).  Split-K over
@@ -43,9 +44,6 @@ namespace {
 #ifndef TLOD_GEMM_PRIO
 #define TLOD_GEMM_PRIO 1
 #endif
-#ifndef TLOD_GEMM_DEPTH3  // three chunks of loads in flight (64-row dgrad tiles, see mainloop)
-#define TLOD_GEMM_DEPTH3 0
-#endif
 #ifndef TLOD_CONV1X1_OCC2  // (see conv_gemm_bs_kernel)
 #define TLOD_CONV1X1_OCC2 1
 #endif
@@ -55,7 +53,15 @@ namespace {
 
 constexpr int kBN = 256, kTK = 16, kNT = 512;
 constexpr int kWM = 2, kWN = 4, kNJ = 2;  // M tile 64*MI (MI = 4 or 3), N tile 256
-constexpr int kPitchK = 48;    // [row][16 k] images
+// [row][16 k] images: 32-B rows, k half h of row r at byte 16 (h ^ bit 3 of r).  The
+// staging ds_write_b64 (16-lane groups = 4 rows x 4 k segments: 128 contiguous bytes) and
+// the fragment reads (ds_read_b128 of one half of 32 rows; ds_read_b64 of 16 rows) then
+// touch every bank once per lane group (tools/lds/banks.py).  Round 4's 48-B pitch had 2-way
+// conflicts on the staging stores: 29% of the <1,1> GEMM's LDS cycles (profiles/r04/pmc_gemm.txt).
+constexpr int kPitchK = 32;
+__device__ __forceinline__ int kimg_off(int row, int half) {
+  return row * kPitchK + 16 * (half ^ ((row >> 3) & 1));
+}
 // MFMA shape: 0 = v_mfma_f32_32x32x16_bf16 (32x32 accumulator tiles), 1 =
 // v_mfma_f32_16x16x16_bf16 (16x16 tiles, same k-step and output tile per wave: the chip can
 // hold a higher clock on the 16x16 shapes, MI355X_MICROARCH.md DVFS give-back item 7)
@@ -90,8 +96,8 @@ struct Stager {
   int off[IT];     // element offset of this lane's 4-vector at chunk 0 (or -1: dead)
   int lds[IT];     // byte offset inside one plane image (-1: no slot)
   int lim[IT];     // for the tail mask: K - k (KC) or R - r (MN)
-  f32x4v r[IT], r2[IT], r3[IT];  // data slots 0 / 1 / 2 (mainloop's prefetch depth)
-  unsigned mask[IT], mask2[IT], mask3[IT];
+  f32x4v r[IT], r2[IT];  // data slots 0 / 1 (mainloop's prefetch depth)
+  unsigned mask[IT], mask2[IT];
   // M/N-contiguous operands only: element (r, k) *= kscale[k] when staged (a frozen BN's
   // scale on the conv weight's output channels, the 1x1 dgrad's K); nullptr: none
   const float* kscale = nullptr;
@@ -111,7 +117,7 @@ struct Stager {
       if (KC) {  // vector idx: row idx/4, k segment 4 (idx & 3)
         const int row = idx >> 2, k4 = (idx & 3) * 4;
         off[i] = slot && r0 + row < R ? (r0 + row) * K + k4 : -1;
-        lds[i] = slot ? row * kPitchK + 2 * k4 : -1;
+        lds[i] = slot ? kimg_off(row, k4 >> 3) + 2 * (k4 & 7) : -1;
         lim[i] = K - k4;
       } else {   // vector idx: k row idx / LPR, columns 4 (idx % LPR)
         const int kr = idx / LPR, c4 = (idx % LPR) * 4;
@@ -123,8 +129,8 @@ struct Stager {
   }
   template <int S = 0>
   __device__ void load(int kc, int R) {
-    f32x4v* rr = S == 2 ? r3 : S ? r2 : r;
-    unsigned* mm = S == 2 ? mask3 : S ? mask2 : mask;
+    f32x4v* rr = S ? r2 : r;
+    unsigned* mm = S ? mask2 : mask;
     kb[S] = kc;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -139,8 +145,8 @@ struct Stager {
   }
   template <int S = 0>
   __device__ void store(unsigned char* img) const {
-    const f32x4v* rr = S == 2 ? r3 : S ? r2 : r;
-    const unsigned* mm = S == 2 ? mask3 : S ? mask2 : mask;
+    const f32x4v* rr = S ? r2 : r;
+    const unsigned* mm = S ? mask2 : mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (lds[i] < 0) continue;
@@ -165,7 +171,7 @@ struct Stager {
 template <int KC>
 __device__ __forceinline__ u32x4 read_operand(const unsigned char* img, int base, int lane) {
   const int l32 = lane & 31, khalf = lane >> 5;
-  if (KC) return *reinterpret_cast<const u32x4*>(img + (base + l32) * kPitchK + 16 * khalf);
+  if (KC) return *reinterpret_cast<const u32x4*>(img + kimg_off(base + l32, khalf));
   // tr reads: lane 4q+p of 16-lane group g supplies row k0+q, columns 4p..4p+3 of the
   // group's 16 columns; it receives its own column's 4 consecutive k
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
@@ -181,7 +187,7 @@ __device__ __forceinline__ u32x4 read_operand(const unsigned char* img, int base
 template <int KC>
 __device__ __forceinline__ u32x2 read_operand16(const unsigned char* img, int base, int lane) {
   const int l16 = lane & 15, g = lane >> 4;
-  if (KC) return *reinterpret_cast<const u32x2*>(img + (base + l16) * kPitchK + 8 * g);
+  if (KC) return *reinterpret_cast<const u32x2*>(img + kimg_off(base + l16, g >> 1) + 8 * (g & 1));
   // tr read: lane 4q+p of group g supplies k row 4g+q, columns base + 4p..4p+3, and receives
   // its own column's 4 consecutive k
   const int q = l16 >> 2, p = l16 & 3;
@@ -250,67 +256,6 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
 #pragma unroll
       for (int r = 0; r < kAccRegs; ++r) acc[i][j][r] = 0.f;
 
-  if constexpr (TLOD_GEMM_DEPTH3 && MI == 1 && !(TLOD_CONV1X1_OCC2 && AK == 1)) {
-    // Three chunks in flight (the depth-2 scheme below with a third register slot): chunk k
-    // of the range lives in slot k % 3 from its load until its split + store; iteration j
-    // stores chunk j + 1 and loads chunk j + 4 into the freed slot.  64-row tiles only: the
-    // 128-row ones spill with a third slot, and the 64-row forward tile runs two workgroups
-    // per CU in a 128-register budget.
-    const int n = c_end - c_begin;
-    sa.template load<0>(c_begin * kTK, Ra);
-    sb.template load<0>(c_begin * kTK, Rb);
-    sa.template load<1>((c_begin + 1) * kTK, Ra);
-    sb.template load<1>((c_begin + 1) * kTK, Rb);
-    sa.template load<2>((c_begin + 2) * kTK, Ra);
-    sb.template load<2>((c_begin + 2) * kTK, Rb);
-    sa.template store<0>(smem);
-    sb.template store<0>(smem + NPL * A_PL);
-    sa.template load<0>((c_begin + 3) * kTK, Ra);
-    sb.template load<0>((c_begin + 3) * kTK, Rb);
-    __syncthreads();
-    auto iter = [&](auto slc, int j) {
-      constexpr int S = decltype(slc)::value;  // slot of chunk j + 1
-      const unsigned char* buf = smem + (j & 1) * BUF;
-      unsigned char* nbuf = smem + ((j + 1) & 1) * BUF;
-      auto mid = [&]() {
-        sa.template store<S>(nbuf);
-        sb.template store<S>(nbuf + NPL * A_PL);
-        sa.template load<S>((c_begin + j + 4) * kTK, Ra);
-        sb.template load<S>((c_begin + j + 4) * kTK, Rb);
-      };
-      if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
-      u32x4 b[kNJ][3];
-#pragma unroll
-      for (int jj = 0; jj < kNJ; ++jj)
-#pragma unroll
-        for (int pl = 0; pl < NPL; ++pl)
-          b[jj][pl] = read_operand<BK>(buf + NPL * A_PL + pl * B_PL, wn * kNJ * 32 + jj * 32, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        if (i == MI / 2) mid();
-        u32x4 a[3];
-#pragma unroll
-        for (int pl = 0; pl < NPL; ++pl)
-          a[pl] = read_operand<AK>(buf + pl * A_PL, wm * MI * 32 + i * 32, lane);
-#pragma unroll
-        for (int jj = 0; jj < kNJ; ++jj)
-          bs_mac<NP>(acc[i][jj], a[0], a[1], a[2], b[jj][0], b[jj][1], b[jj][2]);
-      }
-      if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
-      __syncthreads();
-    };
-    const std::integral_constant<int, 0> S0;
-    const std::integral_constant<int, 1> S1;
-    const std::integral_constant<int, 2> S2;
-    for (int j = 0; j < n; j += 3) {
-      iter(S1, j);
-      if (j + 1 >= n) break;
-      iter(S2, j + 1);
-      if (j + 2 >= n) break;
-      iter(S0, j + 2);
-    }
-    return;
-  }
   if constexpr (TLOD_GEMM_DEPTH2 && MI <= 2) {
     // Two chunks in flight: chunk j of the range sits in data slot j & 1 of the stagers from
     // its load until its split + store, half way through chunk j - 1's MFMAs; the store then
@@ -434,9 +379,9 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
 template <int AK, int BK, int NP, int MI>
 __global__ void __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
-               const float* __restrict__ bias, float* __restrict__ C, float* __restrict__ slab,
-               int M, int N, int K, int tiles_m, int tiles_n, int dp_tiles, int ksplit,
-               int chunks_per_split) {
+               const float* __restrict__ bias, const float* __restrict__ res, int relu,
+               float* __restrict__ C, float* __restrict__ slab, int M, int N, int K, int tiles_m,
+               int tiles_n, int dp_tiles, int ksplit, int chunks_per_split) {
   constexpr int NPL = NP == 6 ? 3 : 2;
   constexpr int BM = kWM * MI * 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -471,24 +416,59 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
   mainloop<AK, BK, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, M, N);
   auto& acc = acc_.t;
 
-  // direct tiles: C (+ bias); tail pieces: tile-local slab (bias added by the reduce)
-  float* St = slab + ((size_t)split * n_tail + ti) * BM * kBN;
+  // direct tiles: C = act(acc + bias + res); tail pieces: tile-local slab (the epilogue is
+  // the reduce's)
+  if (!direct) {
+    float* St = slab + ((size_t)split * n_tail + ti) * BM * kBN;
+#pragma unroll
+    for (int j = 0; j < kAccCols; ++j) {
+      const int nl = wn * kNJ * 32 + acc_col(j, lane);
+#pragma unroll
+      for (int i = 0; i < acc_rows<MI>(); ++i)
+#pragma unroll
+        for (int r = 0; r < kAccRegs; ++r)
+          St[(wm * MI * 32 + acc_row(i, r, lane)) * kBN + nl] = acc[i][j][r];
+    }
+    return;
+  }
+  if (res == nullptr && !relu) {  // (the plain epilogue: a short-K tile's cost is in it)
+#pragma unroll
+    for (int j = 0; j < kAccCols; ++j) {
+      const int n = n0 + wn * kNJ * 32 + acc_col(j, lane);
+      const float bv = bias != nullptr && n < N ? bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < acc_rows<MI>(); ++i)
+#pragma unroll
+        for (int r = 0; r < kAccRegs; ++r) {
+          const int m = m0 + wm * MI * 32 + acc_row(i, r, lane);
+          if (m < M && n < N) C[(size_t)m * N + n] = acc[i][j][r] + bv;
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < kAccCols; ++j) {
-    const int nl = wn * kNJ * 32 + acc_col(j, lane);
-    const int n = n0 + nl;
-    const float bv = direct && bias != nullptr && n < N ? bias[n] : 0.f;
+    const int n = n0 + wn * kNJ * 32 + acc_col(j, lane);
+    const float bv = bias != nullptr && n < N ? bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < acc_rows<MI>(); ++i)
+    for (int i = 0; i < acc_rows<MI>(); ++i) {
+      // a block's residuals loaded together, ahead of its stores (one latency, not one per
+      // element)
+      float ext[kAccRegs];
 #pragma unroll
       for (int r = 0; r < kAccRegs; ++r) {
-        const int ml = wm * MI * 32 + acc_row(i, r, lane);
-        const int m = m0 + ml;
-        if (!direct)
-          St[ml * kBN + nl] = acc[i][j][r];
-        else if (m < M && n < N)
-          C[(size_t)m * N + n] = acc[i][j][r] + bv;
+        const int m = m0 + wm * MI * 32 + acc_row(i, r, lane);
+        ext[r] = res != nullptr && m < M && n < N ? res[(size_t)m * N + n] : 0.f;
       }
+#pragma unroll
+      for (int r = 0; r < kAccRegs; ++r) {
+        const int m = m0 + wm * MI * 32 + acc_row(i, r, lane);
+        float v = acc[i][j][r] + bv;
+        if (res != nullptr) v += ext[r];
+        if (relu) v = fmaxf(v, 0.f);
+        if (m < M && n < N) C[(size_t)m * N + n] = v;
+      }
+    }
   }
 }
 
@@ -496,7 +476,8 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
 // workgroup per (tail tile, 1024 elements).
 __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
     const float* __restrict__ slab, int ksplit, int n_tail, int dp_tiles, int bm, int tiles_m,
-    int M, int N, const float* __restrict__ bias, float* __restrict__ C) {
+    int M, int N, const float* __restrict__ bias, const float* __restrict__ res, int relu,
+    float* __restrict__ C) {
   // a thread takes 4 consecutive slab elements of one row (16-B loads per split piece; one
   // 16-B store when the row is 16-B aligned in C)
   const int tile_elems = bm * kBN;
@@ -521,6 +502,16 @@ __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
     if (n + 1 < N) v.y += bias[n + 1];
     if (n + 2 < N) v.z += bias[n + 2];
     if (n + 3 < N) v.w += bias[n + 3];
+  }
+  if (res) {
+    const float* rr = res + (size_t)m * N + n;
+    v.x += rr[0];
+    if (n + 1 < N) v.y += rr[1];
+    if (n + 2 < N) v.z += rr[2];
+    if (n + 3 < N) v.w += rr[3];
+  }
+  if (relu) {
+    v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
   }
   if (n + 3 < N && ((reinterpret_cast<uintptr_t>(c) & 15) == 0)) {
     *reinterpret_cast<float4*>(c) = v;
@@ -600,7 +591,8 @@ struct Gemm {
     return p.ksplit > 1 ? (size_t)p.ksplit * (tiles - p.dp_tiles) * kBM * kBN * sizeof(float) : 0;
   }
   static int run(const float* A, const float* B, const float* bias, float* C, int M, int N, int K,
-                 float* ws, size_t ws_bytes_, hipStream_t s) {
+                 float* ws, size_t ws_bytes_, hipStream_t s, const float* res = nullptr,
+                 int relu = 0) {
     const TailPlan p = plan(M, N, K);
     if (ws_bytes_ < ws_bytes(M, N, K)) {
       set_error("tlod_gemm_bs_f32: workspace too small");
@@ -615,12 +607,13 @@ struct Gemm {
       attr = true;
     }
     const int nwg = p.dp_tiles + (p.ksplit > 1 ? n_tail * p.ksplit : 0);
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, A, B, bias, C, ws, M, N, K, tiles_m,
-                       tiles_n, p.dp_tiles, p.ksplit, p.cps);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, A, B, bias, res, relu, C, ws, M, N, K,
+                       tiles_m, tiles_n, p.dp_tiles, p.ksplit, p.cps);
     TLOD_LAUNCH_CHECK();
     if (p.ksplit > 1) {
       hipLaunchKernelGGL(gemm_tail_reduce_kernel, dim3(n_tail * (kBM * kBN / 1024)), dim3(256), 0,
-                         s, ws, p.ksplit, n_tail, p.dp_tiles, kBM, tiles_m, M, N, bias, C);
+                         s, ws, p.ksplit, n_tail, p.dp_tiles, kBM, tiles_m, M, N, bias, res, relu,
+                         C);
       TLOD_LAUNCH_CHECK();
     }
     return kOk;
@@ -999,24 +992,6 @@ auto with_conv1x1_gemm(int w_layout, int nprod, int N, int H, int W, int Cout, F
 
 }  // namespace
 
-// gemm_ws.hip: the warp-specialized form (bf16x6)
-bool gemm_ws_applies(int M, int N, int K, int nprod);
-size_t gemm_ws_workspace(int M, int N, int K);
-int gemm_ws_launch(const float* a, const float* b, const float* bias, const float* res, int relu,
-                   float* c, int M, int N, int K, int a_kcontig, int b_kcontig, void* ws,
-                   size_t ws_bytes, hipStream_t s);
-
-// c = act(c + residual) in place (the epilogue of gemm_bs_kernel's callers of the _ex form)
-__global__ void gemm_res_act_kernel(float* __restrict__ c, const float* __restrict__ res, int relu,
-                                    size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    float v = c[i];
-    if (res) v += res[i];
-    if (relu) v = fmaxf(v, 0.f);
-    c[i] = v;
-  }
-}
-
 }  // namespace tlod
 
 using namespace tlod;
@@ -1024,7 +999,6 @@ using namespace tlod;
 extern "C" size_t tlod_gemm_bs_workspace_bytes(int M, int N, int K, int a_kcontig, int b_kcontig,
                                                int nprod) {
   if (M <= 0 || N <= 0 || K <= 0 || (nprod != 3 && nprod != 6)) return 0;
-  if (gemm_ws_applies(M, N, K, nprod)) return gemm_ws_workspace(M, N, K);
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod,
                    [&](auto g) { return g.ws_bytes(M, N, K); });
 }
@@ -1036,9 +1010,6 @@ extern "C" int tlod_gemm_bs_f32(const float* a, const float* b, const float* bia
   TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
   // 32-bit buffer byte offsets
   TLOD_CHECK_ARG((size_t)std::max(M, N) * K * 4 < (1ull << 31), "operand too large");
-  if (gemm_ws_applies(M, N, K, nprod))
-    return gemm_ws_launch(a, b, bias, nullptr, 0, c, M, N, K, a_kcontig, b_kcontig, ws, ws_bytes,
-                          (hipStream_t)stream);
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
     return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   });
@@ -1052,18 +1023,10 @@ extern "C" int tlod_gemm_bs_ex_f32(const float* a, const float* b, const float* 
   TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
   TLOD_CHECK_ARG(residual != c || residual == nullptr, "residual must not alias c");
   TLOD_CHECK_ARG((size_t)std::max(M, N) * K * 4 < (1ull << 31), "operand too large");
-  if (gemm_ws_applies(M, N, K, nprod))
-    return gemm_ws_launch(a, b, bias, residual, relu, c, M, N, K, a_kcontig, b_kcontig, ws,
-                          ws_bytes, (hipStream_t)stream);
-  const int st = with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
-    return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+  return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
+    return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream,
+                 residual, relu);
   });
-  if (st != kOk || (residual == nullptr && !relu)) return st;
-  const size_t n = (size_t)M * N;
-  hipLaunchKernelGGL(gemm_res_act_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)),
-                     dim3(256), 0, (hipStream_t)stream, c, residual, relu, n);
-  TLOD_LAUNCH_CHECK();
-  return kOk;
 }
 
 extern "C" size_t tlod_conv3x3_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
