@@ -466,3 +466,25 @@ def test_bn_scale_folded_into_dgrad_and_wgrad(KS, N, Cin, Cout, H, W):
     assert torch.equal(a, b)
     dw = conv_wgrad(gy, x, KS, math="bf16x6", row_scale=s)
     assert torch.equal(dw, conv_wgrad(gy, x, KS, math="bf16x6") * s.view(-1, 1, 1, 1))
+
+
+@pytest.mark.parametrize("KS,N,Cin,Cout,H,W", [(1, 2, 256, 1024, 19, 38), (3, 2, 256, 256, 19, 38),
+                                              (3, 1, 64, 72, 30, 41),
+                                              # row length Cin * KS * KS = 18 (KS = 1) / 18
+                                              # (KS = 3): float4s of the slab reduce straddle rows
+                                              (1, 1, 18, 2, 9, 13), (3, 1, 2, 2, 9, 13)])
+def test_wgrad_row_scale_accumulate(KS, N, Cin, Cout, H, W):
+    """tlod_conv_wgrad_bs_ex_f32 with accumulate=True and a row scale: out = base + s * dW
+    (the reduce's dW + r * sum), on the 1x1 im2col path, the 3x3 wgrad_ws path, and row
+    lengths that are not a multiple of 4 (round-4 advisor: the scale was taken per float4)."""
+    from tlod.conv import conv_wgrad
+    g = torch.Generator().manual_seed(KS * 1000 + Cin + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g).to(dev)
+    gy = torch.randn(N, Cout, H, W, generator=g).to(dev)
+    s = (torch.rand(Cout, generator=g) + 0.5).to(dev)
+    base = torch.randn(Cout, Cin, KS, KS, generator=g).to(dev)
+    dw = conv_wgrad(gy, x, KS, math="bf16x6")
+    got = conv_wgrad(gy, x, KS, out=base.clone(), accumulate=True, math="bf16x6", row_scale=s)
+    torch.testing.assert_close(got, base + dw * s.view(-1, 1, 1, 1), rtol=1e-6, atol=1e-6)
+    scaled = conv_wgrad(gy, x, KS, math="bf16x6", row_scale=s)
+    assert torch.equal(scaled, dw * s.view(-1, 1, 1, 1))

@@ -69,3 +69,84 @@ def test_limit_per_image():
     assert sum(len(d) for d in out[1:]) == int((allsc >= th).sum()) == 100
     assert all((d[:, 4] >= th).all() for d in out[1:])
     assert limit_per_image(per, 200) is per
+
+
+def _ap_by_detection_loop(dets, gts, ovthresh, use_07):
+    """Independent statement of the VOC metric (voc_eval.py:70-211): walk the detections in
+    descending confidence (np.argsort(-score), as the reference), one at a time."""
+    order = np.argsort(-np.array([d[1] for d in dets]))
+    used = {k: [False] * len(v) for k, v in gts.items()}
+    npos = sum(1 for v in gts.values() for g in v if not g[4])
+    tp, fp = [], []
+    for k in order:
+        img, _, box = dets[k]
+        best, arg = -np.inf, -1
+        for j, g in enumerate(gts[img]):
+            iw = max(min(g[2], box[2]) - max(g[0], box[0]) + 1.0, 0.0)
+            ih = max(min(g[3], box[3]) - max(g[1], box[1]) + 1.0, 0.0)
+            inter = iw * ih
+            ov = inter / ((box[2] - box[0] + 1.0) * (box[3] - box[1] + 1.0) +
+                          (g[2] - g[0] + 1.0) * (g[3] - g[1] + 1.0) - inter)
+            if ov > best:
+                best, arg = ov, j
+        t = f = 0.0
+        if best > ovthresh:
+            if not gts[img][arg][4]:
+                if used[img][arg]:
+                    f = 1.0
+                else:
+                    t, used[img][arg] = 1.0, True
+        else:
+            f = 1.0
+        tp.append(t)
+        fp.append(f)
+    tp, fp = np.cumsum(tp), np.cumsum(fp)
+    rec = tp / float(npos)
+    prec = tp / np.maximum(tp + fp, np.finfo(np.float64).eps)
+    return rec, prec, voc_ap(rec, prec, use_07)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_voc_eval_matches_detection_loop(tmp_path, seed):
+    """tlod.eval.voc.voc_eval (per-image IoU matrices) against the per-detection loop on
+    random scenes: overlapping boxes, tied scores, difficult objects, images without the
+    class, detections in images without ground truth."""
+    from tlod.eval.voc import voc_eval
+    rng = np.random.default_rng(seed)
+    z = np.zeros((8, 8, 3), np.uint8)
+    images, gts, dets = [], {}, []
+    for i in range(12):
+        name = f"im{i:03d}"
+        objs = []
+        for _ in range(int(rng.integers(0, 5))):
+            x1, y1 = rng.integers(1, 150, 2)
+            w, h = rng.integers(5, 60, 2)
+            objs.append(("car" if rng.random() < .8 else "bus", int(x1), int(y1), int(x1 + w),
+                         int(y1 + h), int(rng.random() < .2)))
+        images.append((name, z, objs))
+        gts[name] = [o[1:] for o in objs if o[0] == "car"]
+        for o in objs:  # jittered hits and duplicates, scores on a coarse grid (ties)
+            for _ in range(int(rng.integers(0, 3))):
+                box = np.array(o[1:5], float) + rng.normal(0, 4, 4)
+                dets.append((name, float(rng.integers(0, 20)) / 20, box))
+        for _ in range(int(rng.integers(0, 3))):  # false alarms
+            x1, y1 = rng.uniform(1, 150, 2)
+            dets.append((name, float(rng.integers(0, 20)) / 20, np.array([x1, y1, x1 + 20, y1 + 20])))
+    write_voc(str(tmp_path), images, image_set="test")
+    base = tmp_path / "VOC2007"
+    detfile = tmp_path / "car.txt"
+    with open(detfile, "w") as f:
+        for name, s, b in dets:
+            f.write(f"{name} {s:.3f} {b[0]:.1f} {b[1]:.1f} {b[2]:.1f} {b[3]:.1f}\n")
+    dets = [(n, float(f"{s:.3f}"), np.array([float(f"{v:.1f}") for v in b])) for n, s, b in dets]
+    for use_07 in (True, False):
+        rec, prec, ap = voc_eval(str(detfile), str(base / "Annotations" / "{}.xml"),
+                                 str(base / "ImageSets" / "Main" / "test.txt"), "car", 0.5, use_07)
+        rec2, prec2, ap2 = _ap_by_detection_loop(dets, gts, 0.5, use_07)
+        np.testing.assert_array_equal(rec, rec2)
+        np.testing.assert_array_equal(prec, prec2)
+        assert ap == ap2
+    open(tmp_path / "none.txt", "w").close()  # a class without detections
+    rec, prec, ap = voc_eval(str(tmp_path / "none.txt"), str(base / "Annotations" / "{}.xml"),
+                             str(base / "ImageSets" / "Main" / "test.txt"), "car", 0.5, False)
+    assert rec.size == 0 and prec.size == 0 and ap == 0.0

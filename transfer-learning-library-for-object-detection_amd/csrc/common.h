@@ -39,6 +39,11 @@ enum Status : int {
 
 #define TLOD_LAUNCH_CHECK() TLOD_HIP(hipGetLastError())
 
+// Per-(kernel, device), thread-safe launch facts (runtime.hip): the kernel's dynamic-LDS
+// limit raised to `bytes` once; resident workgroups of the kernel chip-wide.
+hipError_t lds_attr(const void* kern, int bytes);
+int cached_slots(const void* kern, int threads, size_t lds);
+
 inline int div_up(int a, int b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 

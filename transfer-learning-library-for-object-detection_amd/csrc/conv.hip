@@ -1722,9 +1722,12 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, s
       const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * count)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    if (row_scale != nullptr) {  // row_len is a multiple of 4 (checked by the caller)
-      const float r = row_scale[(4 * i) / (size_t)row_len];
-      s.x *= r; s.y *= r; s.z *= r; s.w *= r;
+    if (row_scale != nullptr) {  // per component: a float4 may straddle two rows
+      const size_t e = 4 * i, rl = (size_t)row_len;
+      s.x *= row_scale[e / rl];
+      s.y *= row_scale[(e + 1) / rl];
+      s.z *= row_scale[(e + 2) / rl];
+      s.w *= row_scale[(e + 3) / rl];
       if (accumulate) {
         const float4 o = reinterpret_cast<const float4*>(out)[i];
         s.x = o.x + s.x; s.y = o.y + s.y; s.z = o.z + s.z; s.w = o.w + s.w;
@@ -1934,20 +1937,11 @@ struct FwdPlan {
   }
 };
 
-// Resident workgroup slots of a kernel on this device (occupancy x CUs); callers cache
-// the result per kernel.  Without a device (CPU build checks) assume 256 (1 block/CU).
+// Resident workgroup slots of a kernel on this device (occupancy x CUs), cached per
+// (kernel, device) in runtime.hip.  Without a device (CPU build checks) assume 256.
 template <typename K>
 static int resident_slots(K kern, int threads, size_t lds) {
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess ||
-      per_cu < 1 || cus < 1) {
-    (void)hipGetLastError();
-    return 256;
-  }
-  return per_cu * cus;
+  return cached_slots((const void*)kern, threads, lds);
 }
 
 // Wave quantization: a grid of T whole tiles on S resident slots runs ceil(T/S) rounds,
@@ -1993,7 +1987,7 @@ static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int n
 template <int WM, int WN, int MI, int NJ, int CK, int KS>
 static FwdPlan plan_fwd(int N, int Cin, int H, int W, int Cout) {
   using C = FwdCfg<WM, WN, MI, NJ, CK, KS>;
-  static const int slots = resident_slots(conv_fwd_kernel<WM, WN, MI, NJ, CK, KS, true>, C::NT,
+  const int slots = resident_slots(conv_fwd_kernel<WM, WN, MI, NJ, CK, KS, true>, C::NT,
                                           C::LDS_FLOATS * sizeof(float));
   const int nchunks = div_up(Cin, CK);
   return plan_schedule(div_up(Cout, C::BM), div_up(W, C::TW), div_up(H, C::TH), N, nchunks,
@@ -2014,11 +2008,7 @@ static int launch_fwd(const float* X, const float* Wk, Epi epi, float* Y, int N,
   }
   const size_t lds = C::LDS_FLOATS * sizeof(float);
   auto kern = conv_fwd_kernel<WM, WN, MI, NJ, CK, KS, VEC4>;
-  static bool attr = false;
-  if (!attr) {
-    TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
+  TLOD_HIP(lds_attr((const void*)kern, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wk, epi, Y, N, Cin, H, W,
                      Cout, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps, slab);
   TLOD_LAUNCH_CHECK();
@@ -2122,7 +2112,7 @@ static WsTile ws_tile(int H, int W, bool pool) {
 
 template <int WM, int WN, int MI, int NJ, int NP>
 static int ws_slots() {
-  static const int slots = resident_slots(conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>,
+  const int slots = resident_slots(conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>,
                                           WM * WN * 64 + kProdWaves * 64,
                                           WsCfg<WM, WN, MI, NJ, NP>::LDS_BYTES);
   return slots;
@@ -2131,7 +2121,7 @@ static int ws_slots() {
 template <int WM, int WN, int MI, int NJ, int NP, bool BAND>
 static FwdPlan plan_fwd_bs(int N, int Cin, int H, int W, int Cout, bool allow_split = true) {
   using C = BsCfg<WM, WN, MI, NJ, NP, BAND>;
-  static const int slots_plain = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>,
+  const int slots_plain = resident_slots(conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>,
                                                 C::NT, C::LDS_BYTES);
   int slots = slots_plain;
   WsTile wt{C::TH, C::TW};
@@ -2176,12 +2166,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
     if (use_ws(Cin, Cout, H, W)) {
       using WC = WsCfg<WM, WN, MI, NJ, NP>;
       auto kern = conv_fwd_bs_ws_kernel<WM, WN, MI, NJ, NP>;
-      static bool attr = false;
-      if (!attr) {
-        TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)WC::LDS_BYTES));
-        attr = true;
-      }
+      TLOD_HIP(lds_attr((const void*)kern, (int)WC::LDS_BYTES));
       hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT + kProdWaves * 64), WC::LDS_BYTES,
                          s, X, Wp, epi, Y, N, Cin, H, W, Cout, p.tiles_m, p.tiles_w, p.tiles_h,
                          p.dp_tiles, p.ksplit, p.cps, slab, p.th, p.tw);
@@ -2191,11 +2176,7 @@ static int launch_fwd_bs(const float* X, const unsigned short* Wp, Epi epi, floa
   if (!launched) {
     const size_t lds = C::LDS_BYTES;
     auto kern = conv_fwd_bs_kernel<WM, WN, MI, NJ, NP, BAND>;
-    static bool attr = false;
-    if (!attr) {
-      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr = true;
-    }
+    TLOD_HIP(lds_attr((const void*)kern, (int)lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), lds, s, X, Wp, epi, Y, N, Cin, H, W,
                        Cout, p.tiles_m, p.tiles_w, p.tiles_h, p.dp_tiles, p.ksplit, p.cps, slab);
   }
@@ -2267,7 +2248,7 @@ struct Wgrad {
   static int splits(int N, int Cin, int H, int W, int Cout) {
     const int tiles = div_up(Cout, C::BM) * div_up(Cin * C::KK, C::BN);
     const int chunks = N * div_up(H, C::TH) * div_up(W, C::TW);
-    static const int slots =
+    const int slots =
         resident_slots(conv_wgrad_kernel<WM, WN, MI, NJ, KS, TH>, C::NT, kLds);
     return pick_splits(tiles, chunks, slots);
   }
@@ -2279,11 +2260,7 @@ struct Wgrad {
     const int cps = div_up(total_chunks, splits);
     const int nwg = tiles_m * tiles_n * splits;
     auto kern = conv_wgrad_kernel<WM, WN, MI, NJ, KS, TH>;
-    static bool attr = false;
-    if (!attr) {
-      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-      attr = true;
-    }
+    TLOD_HIP(lds_attr((const void*)kern, (int)kLds));
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), kLds, s, G, X, slab, N, Cin, H, W, Cout,
                        tiles_m, tiles_n, splits, cps);
     TLOD_LAUNCH_CHECK();
@@ -2331,7 +2308,7 @@ template <int WM, int WN, int MI, int NJ, int KS, int NP>
 struct WgradBs {
   using C = WgBsCfg<WM, WN, MI, NJ, NP>;
   static int splits(int N, int Cin, int H, int W, int Cout, double* t_out = nullptr) {
-    static const int slots =
+    const int slots =
         resident_slots(conv_wgrad_bs_kernel<WM, WN, MI, NJ, KS, NP>, C::NT, C::LDS_BYTES);
     const long long tiles = (long long)div_up(Cout, C::BM) * div_up(Cin * KS * KS, C::BN);
     const int chunks = N * div_up(H * W, C::TK);
@@ -2349,11 +2326,7 @@ struct WgradBs {
     const long long nwg = (long long)tiles_m * tiles_n * splits;
     TLOD_CHECK_ARG(nwg < (1ll << 31), "grid too large");
     auto kern = conv_wgrad_bs_kernel<WM, WN, MI, NJ, KS, NP>;
-    static bool attr = false;
-    if (!attr) {
-      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES));
-      attr = true;
-    }
+    TLOD_HIP(lds_attr((const void*)kern, C::LDS_BYTES));
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(C::NT), C::LDS_BYTES, s, G, X, slab, N, Cin,
                        H, W, Cout, tiles_m, tiles_n, splits, cps, 1.0f / (float)W, db_slab);
     TLOD_LAUNCH_CHECK();

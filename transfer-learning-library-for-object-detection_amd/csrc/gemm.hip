@@ -27,7 +27,6 @@
 
 #include <algorithm>
 #include <type_traits>
-#include <unordered_map>
 
 namespace tlod {
 
@@ -527,20 +526,7 @@ __global__ void __launch_bounds__(256) gemm_tail_reduce_kernel(
 // function-pointer type, so a per-type static would mix kernels of different occupancy)
 template <typename K>
 int slots_of(K kern, size_t lds) {
-  static std::unordered_map<const void*, int> cache;
-  const auto hit = cache.find((const void*)kern);
-  if (hit != cache.end()) return hit->second;
-  int& cached = cache[(const void*)kern];
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kNT, lds) != hipSuccess ||
-      per_cu < 1 || cus < 1) {
-    (void)hipGetLastError();
-    return cached = 256;
-  }
-  return cached = per_cu * cus;
+  return cached_slots((const void*)kern, kNT, lds);
 }
 
 struct TailPlan {
@@ -601,11 +587,7 @@ struct Gemm {
     const int tiles_m = div_up(M, kBM), tiles_n = div_up(N, kBN);
     const int n_tail = tiles_m * tiles_n - p.dp_tiles;
     auto kern = gemm_bs_kernel<AK, BK, NP, MI>;
-    static bool attr = false;
-    if (!attr) {
-      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-      attr = true;
-    }
+    TLOD_HIP(lds_attr((const void*)kern, (int)kLds));
     const int nwg = p.dp_tiles + (p.ksplit > 1 ? n_tail * p.ksplit : 0);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, A, B, bias, res, relu, C, ws, M, N, K,
                        tiles_m, tiles_n, p.dp_tiles, p.ksplit, p.cps);
@@ -930,11 +912,7 @@ struct ConvGemm {
     const int tiles_m = div_up(Cout, kBM), tiles_n = div_up(H * W, kBN);
     const int n_tail = tiles_m * tiles_n * N - p.dp_tiles;
     auto kern = conv_gemm_bs_kernel<AK, NP, MI, KS>;
-    static bool attr = false;
-    if (!attr) {
-      TLOD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-      attr = true;
-    }
+    TLOD_HIP(lds_attr((const void*)kern, (int)kLds));
     const int nwg = p.dp_tiles + (p.ksplit > 1 ? n_tail * p.ksplit : 0);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, X, Wt, epi, Y, ws, N, C, H, W, Cout,
                        tiles_m, tiles_n, p.dp_tiles, p.ksplit, p.cps);

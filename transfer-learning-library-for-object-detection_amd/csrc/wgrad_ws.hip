@@ -618,12 +618,7 @@ int wgrad_ws_launch(const float* dy, const float* x, float* dw, float* db, int a
                                                  align_up((size_t)p.splits * tiles * TILE_FLOATS *
                                                               sizeof(float), 16))
                       : nullptr;
-  static bool attr = false;
-  if (!attr) {
-    TLOD_HIP(hipFuncSetAttribute((const void*)wgrad_ws_kernel,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    attr = true;
-  }
+  TLOD_HIP(lds_attr((const void*)wgrad_ws_kernel, LDS_BYTES));
   hipLaunchKernelGGL(wgrad_ws_kernel, dim3((unsigned)(tiles * p.splits)), dim3(NT), LDS_BYTES, s,
                      dy, x, slab, db_slab, N, Cin, H, W, Cout, p.tiles_m, p.tiles_c, p.splits,
                      p.cps);

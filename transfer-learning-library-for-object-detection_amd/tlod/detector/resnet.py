@@ -32,14 +32,18 @@ from ..linear import LinearActFunction, LinearFunction, linear_math
 def fold_bn(bn):
     """Frozen eval-mode BatchNorm as y = x * scale + shift (per channel).  Cached on the
     module and recomputed only when one of its four tensors changes: a different tensor object
-    (reassignment, load_state_dict(assign=True)), an in-place write (its version counter) or
-    a write that bypasses it (tlod.conv.weights_updated: the data-parallel broadcast).
+    (reassignment, load_state_dict(assign=True)), new storage under the same object
+    (module.to() / .cuda(): param.data = ...), an in-place write (its version counter) or a
+    write that bypasses it (tlod.conv.weights_updated: the data-parallel broadcast).
     The cache holds the four tensors themselves, so a replaced tensor's storage cannot be
     reused at the same address while its fold is cached.  ResNet101 has 104 BatchNorms, i.e.
     400+ small launches per forward otherwise."""
     assert not bn.weight.requires_grad, "tlod ResNet expects frozen BatchNorm (resnet.py:261-267)"
     ts = (bn.weight, bn.bias, bn.running_mean, bn.running_var)
-    vs = tuple(t._version for t in ts) + (bn.eps, conv_mod._EXTERNAL_WRITES[0])
+    # (data_ptr / device / dtype: module.to() and .cuda() swap a parameter's storage through
+    # param.data = ..., which keeps the object and its version counter)
+    vs = tuple((t._version, t.data_ptr(), t.device, t.dtype) for t in ts) + (
+        bn.eps, conv_mod._EXTERNAL_WRITES[0])
     c = getattr(bn, "_tlod_fold", None)
     if c is not None and c[1] == vs and all(a is b for a, b in zip(c[0], ts)):
         return c[2], c[3]

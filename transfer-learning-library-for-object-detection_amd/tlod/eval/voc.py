@@ -1,8 +1,15 @@
-"""PASCAL VOC detection AP (lib/datasets/voc_eval.py:15-211), the reference's Python eval.
+"""PASCAL VOC detection AP — the metric of lib/datasets/voc_eval.py:15-211 (MIT), restated.
 
-Host-side numpy, as in the reference (it reads the comp4 results files the test driver
-wrote, lib/datasets/pascal_voc.py:284-298).  The annotation pickle cache of the reference
-(voc_eval.py:110-128) is not kept: annotations are parsed each call.
+Same numbers as the reference's per-class evaluation (greedy matching of detections in
+descending confidence to the highest-IoU ground truth of their image at IoU > ovthresh,
+difficult objects neither counted nor penalised, a ground truth matched at most once;
+VOC07 11-point or area-under-envelope AP), organised differently: annotations are parsed
+into arrays once per image, detections are grouped per image and each image's IoU matrix
+is computed in one broadcast, so the only Python loop left is the greedy assignment itself.
+The reference's annotation pickle cache (voc_eval.py:110-128) is not kept.
+
+Host-side numpy: it reads the comp4 result files the test driver writes
+(lib/datasets/pascal_voc.py:284-298), off the device path.
 """
 import xml.etree.ElementTree as ET
 
@@ -10,94 +17,110 @@ import numpy as np
 
 
 def parse_rec(filename):
-    """voc_eval.py:15-33."""
-    tree = ET.parse(filename)
-    objects = []
-    for obj in tree.findall("object"):
-        o = {"name": obj.find("name").text}
-        if obj.find("pose") is not None:
-            o["pose"] = obj.find("pose").text
-        o["truncated"] = int(obj.find("truncated").text)
-        o["difficult"] = int(obj.find("difficult").text)
-        bbox = obj.find("bndbox")
-        o["bbox"] = [int(bbox.find(k).text) for k in ("xmin", "ymin", "xmax", "ymax")]
-        objects.append(o)
-    return objects
+    """Objects of one VOC annotation file: dicts with name, pose, truncated, difficult and
+    the 1-based integer bbox [xmin, ymin, xmax, ymax] (voc_eval.py:15-33)."""
+    out = []
+    for node in ET.parse(filename).findall("object"):
+        box = node.find("bndbox")
+        rec = {"name": node.find("name").text,
+               "truncated": int(node.find("truncated").text),
+               "difficult": int(node.find("difficult").text),
+               "bbox": [int(box.find(tag).text) for tag in ("xmin", "ymin", "xmax", "ymax")]}
+        pose = node.find("pose")
+        if pose is not None:
+            rec["pose"] = pose.text
+        out.append(rec)
+    return out
 
 
 def voc_ap(rec, prec, use_07_metric=False):
-    """voc_eval.py:36-67: VOC07 11-point AP, or the area under the precision envelope."""
+    """AP from recall / precision curves (voc_eval.py:36-67): the mean of the maximum
+    precision at recall >= 0, 0.1, ..., 1 (VOC07), or the area under the monotone
+    precision envelope summed where recall changes."""
+    rec = np.asarray(rec, dtype=np.float64)
+    prec = np.asarray(prec, dtype=np.float64)
     if use_07_metric:
-        ap = 0.0
-        for t in np.arange(0.0, 1.1, 0.1):
-            p = 0 if np.sum(rec >= t) == 0 else np.max(prec[rec >= t])
-            ap = ap + p / 11.0
-        return ap
-    mrec = np.concatenate(([0.0], rec, [1.0]))
-    mpre = np.concatenate(([0.0], prec, [0.0]))
-    for i in range(mpre.size - 1, 0, -1):
-        mpre[i - 1] = np.maximum(mpre[i - 1], mpre[i])
-    i = np.where(mrec[1:] != mrec[:-1])[0]
-    return np.sum((mrec[i + 1] - mrec[i]) * mpre[i + 1])
+        total = 0.0
+        for t in np.arange(0.0, 1.1, 0.1):  # accumulated in the reference's order
+            hit = rec >= t
+            total = total + (np.max(prec[hit]) if hit.any() else 0) / 11.0
+        return total
+    r = np.concatenate(([0.0], rec, [1.0]))
+    envelope = np.maximum.accumulate(np.concatenate(([0.0], prec, [0.0]))[::-1])[::-1]
+    steps = np.flatnonzero(r[1:] != r[:-1])
+    return np.sum((r[steps + 1] - r[steps]) * envelope[steps + 1])
+
+
+def _iou_matrix(det, gt):
+    """IoU of every (detection, ground truth) pair with the reference's +1 pixel areas,
+    elementwise the same float64 operations as voc_eval.py:165-180."""
+    lo_x = np.maximum(gt[None, :, 0], det[:, None, 0])
+    lo_y = np.maximum(gt[None, :, 1], det[:, None, 1])
+    hi_x = np.minimum(gt[None, :, 2], det[:, None, 2])
+    hi_y = np.minimum(gt[None, :, 3], det[:, None, 3])
+    inter = np.maximum(hi_x - lo_x + 1.0, 0.0) * np.maximum(hi_y - lo_y + 1.0, 0.0)
+    det_area = (det[:, 2] - det[:, 0] + 1.0) * (det[:, 3] - det[:, 1] + 1.0)
+    gt_area = (gt[:, 2] - gt[:, 0] + 1.0) * (gt[:, 3] - gt[:, 1] + 1.0)
+    return inter / (det_area[:, None] + gt_area[None, :] - inter)
+
+
+def _read_detections(detpath):
+    """(image ids, confidences, boxes) of a comp4 results file: "<image> <score> <x1> <y1>
+    <x2> <y2>" per line."""
+    with open(detpath) as f:
+        fields = [line.strip().split(" ") for line in f]
+    ids = [row[0] for row in fields]
+    scores = np.array([float(row[1]) for row in fields])
+    boxes = np.array([[float(v) for v in row[2:]] for row in fields], dtype=np.float64).reshape(-1, 4)
+    return ids, scores, boxes
 
 
 def voc_eval(detpath, annopath, imagesetfile, classname, ovthresh=0.5, use_07_metric=False):
-    """voc_eval.py:70-211 -> (rec, prec, ap) for one class.  detpath: the class's results
-    file ("<image> <score> <x1> <y1> <x2> <y2>" per line, 1-based); annopath: a format
-    string of the annotation path per image name."""
+    """(rec, prec, ap) of one class (voc_eval.py:70-211).  detpath: the class's results
+    file; annopath: a format string of the annotation path per image name."""
     with open(imagesetfile) as f:
-        imagenames = [x.strip() for x in f.readlines()]
-    recs = {name: parse_rec(annopath.format(name)) for name in imagenames}
-    class_recs = {}
+        names = [line.strip() for line in f]
+    gt_box, gt_hard = {}, {}
     npos = 0
-    for name in imagenames:
-        R = [o for o in recs[name] if o["name"] == classname]
-        bbox = np.array([x["bbox"] for x in R])
-        difficult = np.array([x["difficult"] for x in R]).astype(bool)
-        npos = npos + sum(~difficult)
-        class_recs[name] = {"bbox": bbox, "difficult": difficult, "det": [False] * len(R)}
-    with open(detpath) as f:
-        lines = f.readlines()
-    splitlines = [x.strip().split(" ") for x in lines]
-    image_ids = [x[0] for x in splitlines]
-    confidence = np.array([float(x[1]) for x in splitlines])
-    BB = np.array([[float(z) for z in x[2:]] for x in splitlines])
-    nd = len(image_ids)
+    for name in names:
+        objs = [o for o in parse_rec(annopath.format(name)) if o["name"] == classname]
+        gt_box[name] = np.array([o["bbox"] for o in objs], dtype=np.float64).reshape(-1, 4)
+        gt_hard[name] = np.array([bool(o["difficult"]) for o in objs], dtype=bool)
+        npos += int((~gt_hard[name]).sum())
+
+    ids, scores, boxes = _read_detections(detpath)
+    nd = len(ids)
     tp = np.zeros(nd)
     fp = np.zeros(nd)
-    if BB.shape[0] > 0:
-        sorted_ind = np.argsort(-confidence)
-        BB = BB[sorted_ind, :]
-        image_ids = [image_ids[x] for x in sorted_ind]
-        for d in range(nd):
-            R = class_recs[image_ids[d]]
-            bb = BB[d, :].astype(float)
-            ovmax = -np.inf
-            BBGT = R["bbox"].astype(float)
-            if BBGT.size > 0:
-                ixmin = np.maximum(BBGT[:, 0], bb[0])
-                iymin = np.maximum(BBGT[:, 1], bb[1])
-                ixmax = np.minimum(BBGT[:, 2], bb[2])
-                iymax = np.minimum(BBGT[:, 3], bb[3])
-                iw = np.maximum(ixmax - ixmin + 1.0, 0.0)
-                ih = np.maximum(iymax - iymin + 1.0, 0.0)
-                inters = iw * ih
-                uni = ((bb[2] - bb[0] + 1.0) * (bb[3] - bb[1] + 1.0)
-                       + (BBGT[:, 2] - BBGT[:, 0] + 1.0) * (BBGT[:, 3] - BBGT[:, 1] + 1.0) - inters)
-                overlaps = inters / uni
-                ovmax = np.max(overlaps)
-                jmax = np.argmax(overlaps)
-            if ovmax > ovthresh:
-                if not R["difficult"][jmax]:
-                    if not R["det"][jmax]:
-                        tp[d] = 1.0
-                        R["det"][jmax] = 1
-                    else:
-                        fp[d] = 1.0
-            else:
-                fp[d] = 1.0
-    fp = np.cumsum(fp)
-    tp = np.cumsum(tp)
-    rec = tp / float(npos)
-    prec = tp / np.maximum(tp + fp, np.finfo(np.float64).eps)
+    if nd:
+        order = np.argsort(-scores)  # the reference's call: the same order for ties
+        ranked_ids = [ids[k] for k in order]
+        ranked_boxes = boxes[order].astype(float)
+        by_image = {}
+        for rank, name in enumerate(ranked_ids):
+            by_image.setdefault(name, []).append(rank)
+        for name, ranks in by_image.items():
+            ranks = np.array(ranks)
+            gts = gt_box[name]
+            if gts.shape[0] == 0:  # no ground truth of the class in this image
+                fp[ranks] = 1.0
+                continue
+            iou = _iou_matrix(ranked_boxes[ranks], gts)
+            best = iou.argmax(axis=1)
+            best_iou = iou[np.arange(len(ranks)), best]
+            taken = np.zeros(gts.shape[0], dtype=bool)
+            for rank, j, ov in zip(ranks, best, best_iou):  # greedy, in confidence order
+                if not ov > ovthresh:
+                    fp[rank] = 1.0
+                elif gt_hard[name][j]:
+                    continue
+                elif taken[j]:
+                    fp[rank] = 1.0
+                else:
+                    tp[rank] = 1.0
+                    taken[j] = True
+    ctp = np.cumsum(tp)
+    cfp = np.cumsum(fp)
+    rec = ctp / float(npos)
+    prec = ctp / np.maximum(ctp + cfp, np.finfo(np.float64).eps)
     return rec, prec, voc_ap(rec, prec, use_07_metric)
