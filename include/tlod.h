@@ -98,6 +98,23 @@ int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, int H, int W
                                const float* rois, int R, int ph, int pw, float scale,
                                float* bottom_grad, void* ws, size_t ws_bytes,
                                tlod_stream_t stream);
+/* ResNet RoI-head entry: RoIAlignAvg's bins (2i, 2j) only, channels-last — what
+ * RCNN_top = layer4 reads of pool5 (its first bottleneck subsamples by 2:
+ * lib/DAF/resnet.py:64-102, :286-288 via _head_to_tail).  out (R, QH, QW, C) with
+ * QH = ceil(ph / 2), QW = ceil(pw / 2), equal bit for bit to
+ * tlod_roi_align_avg_fwd_f32's out[r][c][2i][2j]; the backward ADDS the gradient of that
+ * selection into bottom_grad (B,C,H,W), deterministic (the sorted-tap gather), equal to
+ * tlod_roi_align_avg_bwd_f32 of a top gradient that is zero off the selected bins.  One
+ * workspace query covers both directions. */
+size_t tlod_roi_align_avg_s2_workspace_bytes(int B, int C, int H, int W, int R, int ph, int pw);
+int tlod_roi_align_avg_s2_nhwc_fwd_f32(const float* feat, int B, int C, int H, int W,
+                                       const float* rois, int R, int ph, int pw, float scale,
+                                       float* out, void* ws, size_t ws_bytes,
+                                       tlod_stream_t stream);
+int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, int C, int H, int W,
+                                       const float* rois, int R, int ph, int pw, float scale,
+                                       float* bottom_grad, void* ws, size_t ws_bytes,
+                                       tlod_stream_t stream);
 
 /* ------------------------------------------------------------------ RoIPool
  * Replaces: roi_pooling_forward_cuda / roi_pooling_backward_cuda

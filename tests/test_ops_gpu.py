@@ -137,6 +137,38 @@ def test_roi_align_avg_bwd_gather(B, C, H, W, R, P, monkeypatch):
     np.testing.assert_allclose(a, ref, rtol=1e-5, atol=atol)
 
 
+@pytest.mark.parametrize("B,C,H,W,R,P", [(2, 1024, 38, 75, 600, 7), (1, 40, 20, 30, 90, 7),
+                                         (2, 300, 12, 16, 33, 6), (2, 16, 6, 5, 17, 5),
+                                         (1, 70, 20, 30, -300, 7), (1, 8, 10, 12, 5, 1)])
+def test_roi_head_entry_matches_roi_align_avg(B, C, H, W, R, P, monkeypatch):
+    """The ResNet RoI head's entry (tlod_roi_align_avg_s2_nhwc_*: bins (2i, 2j), channels-last)
+    against the fused RoIAlignAvg -> permute -> stride-2 subsample it replaces, forward and
+    backward bit for bit (both backwards on the sorted-tap gather: the same taps in the same
+    order); even P leaves the last sample row / column without a bin; R = -300: one small
+    RoI 300 times (runs across many tap segments); (2, 16, 6, 5): RoIs past the map."""
+    from tlod.roi_align import RoIAlignAvgFunction, roi_align_avg_s2_nhwc
+    monkeypatch.setenv("TLOD_ROI_BWD_GATHER", "1")
+    rng = np.random.default_rng(abs(R) + P + C)
+    f = torch.from_numpy(_feat(rng, B, C, H, W)).to(dev)
+    if R < 0:
+        r = np.tile(np.array([[0, 100.0, 90.0, 130.0, 121.0]], np.float32), (-R, 1))
+        R = -R
+    else:
+        r = _rois(rng, R, B, W * 16 + 200, H * 16 + 200)
+    rt = torch.from_numpy(r).to(dev)
+    Q = (P + 1) // 2
+    g = torch.from_numpy(rng.standard_normal((R, Q, Q, C)).astype(np.float32)).to(dev)
+    fa = f.clone().requires_grad_(True)
+    got = roi_align_avg_s2_nhwc(fa, rt, P, P, 1.0 / 16)
+    fb = f.clone().requires_grad_(True)
+    ref = RoIAlignAvgFunction.apply(fb, rt, P, P, 1.0 / 16).permute(0, 2, 3, 1)[:, ::2, ::2, :]
+    assert got.shape == (R, Q, Q, C) and got.is_contiguous()
+    assert torch.equal(got, ref)
+    got.backward(g)
+    ref.backward(g)
+    assert torch.equal(fa.grad, fb.grad)
+
+
 @pytest.mark.parametrize("B,C,H,W,R", [(1, 64, 37, 62, 128), (2, 16, 20, 25, 40)])
 def test_roi_pool_fwd_bwd(B, C, H, W, R):
     from tlod.roi_pool import roi_pool_with_argmax

@@ -258,12 +258,16 @@ __global__ void __launch_bounds__(kNhwcThreads) roi_align_avg_bwd_nhwc_kernel(
 // sg 73 MB written and read once per tap (~290 MB, mostly L2 / Infinity-Cache hits),
 // bottom_grad 11 MB read + written.
 
+// (sy_lim, sx_lim: samples at rows >= sy_lim or columns >= sx_lim feed no output bin — the
+// stride-2 head entry's bins (2i, 2j) leave the last sample row / column of an even bin
+// count uncovered — and get the sentinel key like samples outside the map)
 __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__ rois, int R,
                                                        float scale, int H, int W, int ph, int pw,
                                                        unsigned ncell,
                                                        unsigned* __restrict__ keys,
                                                        unsigned* __restrict__ vals,
-                                                       float2* __restrict__ geo) {
+                                                       float2* __restrict__ geo, int sy_lim,
+                                                       int sx_lim) {
   const int ah = ph + 1, aw = pw + 1, S = ah * aw;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R * S) return;
@@ -274,7 +278,7 @@ __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__
   bool vy, vx;
   align_axis(ro[2] * scale, ro[4] * scale, ah, sy, H, &y, &hr, &vy);
   align_axis(ro[1] * scale, ro[3] * scale, aw, sx, W, &x, &wr, &vx);
-  const bool ok = vy && vx;
+  const bool ok = vy && vx && sy < sy_lim && sx < sx_lim;
   const unsigned c00 = (unsigned)(((int)ro[0] * H + y) * W + x);
   geo[i] = make_float2(hr, wr);
 #pragma unroll
@@ -336,11 +340,16 @@ __device__ __forceinline__ float tap_value(float g, float hr, float wr, int k) {
 // grid (ceil(nseg / 4), ceil(C / 64)), 4 waves: wave = segment of 64 sorted taps, lane =
 // channel.  flags[seg]: 1 = owns a run continuing into the next segments (its tail piece in
 // carry_tail), 2 = one run covering the whole segment and continuing on both sides.
+// S2 (the stride-2 head entry): no sample-gradient rows — sample (r, sy, sx) feeds exactly
+// one output bin, so its gradient is that bin's top row / 4, read straight from the
+// channels-last top gradient (R, QH, QW, C) (S = samples per RoI, aw = samples per row).
+template <bool S2>
 __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
     const int* __restrict__ start, const unsigned* __restrict__ keys,
     const unsigned* __restrict__ vals, const float2* __restrict__ geo,
     const float* __restrict__ sg, int C, int ncell, float* __restrict__ acc,
-    float* __restrict__ carry_head, float* __restrict__ carry_tail, int* __restrict__ flags) {
+    float* __restrict__ carry_head, float* __restrict__ carry_tail, int* __restrict__ flags,
+    int S, int aw, int QH, int QW) {
   const int lane = threadIdx.x & 63;
   const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = start[ncell];  // valid taps (sorted to the front)
@@ -378,7 +387,13 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
 #pragma unroll
     for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
       const unsigned vu = __builtin_amdgcn_readlane(vl, min(j + u, jn - 1));
-      sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
+      if constexpr (S2) {
+        const int row = (int)(vu >> 2), r = row / S, smp = row - r * S;
+        const int trow = (r * QH + (smp / aw >> 1)) * QW + ((smp % aw) >> 1);
+        sv[u] = cok ? sg[(size_t)trow * C + c] * 0.25f : 0.f;  // = top / 4.f exactly
+      } else {
+        sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
+      }
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -447,7 +462,8 @@ struct RbgWs {
   size_t cub_bytes;
 };
 
-static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, int ph, int pw) {
+static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, int ph, int pw,
+                        bool s2 = false) {
   const size_t S = (size_t)(ph + 1) * (pw + 1), n = (size_t)R * S * 4;
   w.keys = cv.take<unsigned>(n);
   w.vals = cv.take<unsigned>(n);
@@ -455,7 +471,7 @@ static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, 
   w.vals_s = cv.take<unsigned>(n);
   w.geo = cv.take<float2>((size_t)R * S);
   w.start = cv.take<int>((size_t)B * H * W + 1);
-  w.sg = cv.take<float>((size_t)R * S * C);
+  w.sg = s2 ? nullptr : cv.take<float>((size_t)R * S * C);
   const size_t nseg = (n + 63) / 64;
   w.acc = cv.take<float>((size_t)B * H * W * C);
   w.carry_head = cv.take<float>(nseg * C);
@@ -493,6 +509,87 @@ __global__ void __launch_bounds__(256) nhwc_add_to_nchw_kernel(const float* __re
     const int c = c0 + i, p = p0 + tx;
     if (p < HW && c < C) o[(size_t)c * HW + p] += tile[tx][i];
   }
+}
+
+// ------------------------------------------------------------ ResNet RoI-head entry
+// RCNN_top = layer4, whose first bottleneck subsamples by 2 (lib/DAF/resnet.py:64-102,
+// :286-288): of RoIAlignAvg's ph x pw bins it reads only (2i, 2j), channels-last.  So the
+// head entry computes exactly those bins, (R, QH, QW, C) with QH = ceil(ph / 2), from a
+// channels-last copy of the feature map (every bilinear tap a coalesced row of channels;
+// the NCHW kernel's lanes each read a different plane), and none of the 7 x 7 map, its
+// permute to channels-last or the strided subsample copy is materialised.  Values are the
+// fused NCHW kernel's bit for bit (same samples, same average order).  The bins (2i, 2j)
+// cover disjoint 2 x 2 sample blocks, so the backward gives each sample its bin's top / 4
+// with no sample-gradient pass (rbg_seg_gather_kernel<true>).
+
+// out (B, HW, C) = in (B, C, HW): 64 x 64 tiles through LDS
+__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ in, int C,
+                                                           int HW, float* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z, p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const float* a = in + (size_t)b * C * HW;
+  float* o = out + (size_t)b * HW * C;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, p = p0 + tx;
+    tile[i][tx] = (p < HW && c < C) ? a[(size_t)c * HW + p] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int p = p0 + i, c = c0 + tx;
+    if (p < HW && c < C) o[(size_t)p * C + c] = tile[tx][i];
+  }
+}
+
+// align_sample on a channels-last map (row pitch W * C, column pitch C)
+__device__ __forceinline__ float align_sample_nhwc(const float* __restrict__ base, int W, int C,
+                                                   int y, int x, float hr, float wr) {
+  const float* p = base + ((size_t)y * W + x) * C;
+  const float ul = p[0], ur = p[C];
+  const float dl = p[(size_t)W * C], dr = p[(size_t)W * C + C];
+  double t1 = ((double)ul * (1. - (double)hr)) * (1. - (double)wr);
+  double t2 = ((double)ur * (1. - (double)hr)) * (double)wr;
+  double t3 = (double)(dl * hr) * (1. - (double)wr);
+  double t4 = (double)((dr * hr) * wr);
+  return (float)(((t1 + t2) + t3) + t4);
+}
+
+// grid (R, ceil(C / 256)): thread = channel; out (R, QH, QW, C)
+__global__ void __launch_bounds__(256) roi_align_avg_s2_fwd_kernel(
+    const float* __restrict__ feat_nhwc, float scale, int C, int H, int W, int ph, int pw,
+    const float* __restrict__ rois, float* __restrict__ out) {
+  const int ah = ph + 1, aw = pw + 1, QH = (ph + 1) / 2, QW = (pw + 1) / 2;
+  const int r = blockIdx.x, t = threadIdx.x, c = blockIdx.y * 256 + t;
+  __shared__ int gy[8], gx[8];
+  __shared__ float ghr[8], gwr[8];
+  __shared__ bool gvy[8], gvx[8];
+  const float* ro = rois + r * 5;
+  if (t < ah) align_axis(ro[2] * scale, ro[4] * scale, ah, t, H, &gy[t], &ghr[t], &gvy[t]);
+  if (t >= 32 && t < 32 + aw) {
+    const int p = t - 32;
+    align_axis(ro[1] * scale, ro[3] * scale, aw, p, W, &gx[p], &gwr[p], &gvx[p]);
+  }
+  __syncthreads();
+  if (c >= C) return;
+  const float* base = feat_nhwc + (size_t)(int)ro[0] * H * W * C + c;
+  float* o = out + (size_t)r * QH * QW * C + c;
+  for (int i = 0; i < QH; ++i)
+    for (int j = 0; j < QW; ++j) {
+      float sv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sy = 2 * i + (k >> 1), sx = 2 * j + (k & 1);
+        sv[k] = gvy[sy] && gvx[sx] ? align_sample_nhwc(base, W, C, gy[sy], gx[sx], ghr[sy], gwr[sx])
+                                   : 0.f;
+      }
+      // avg_pool2d(2, s1) as roi_align_avg_fwd_kernel: ((((0+a)+b)+c)+d)/4
+      float acc = 0.f;
+      acc += sv[0];
+      acc += sv[1];
+      acc += sv[2];
+      acc += sv[3];
+      o[(size_t)(i * QW + j) * C] = acc / 4.f;
+    }
 }
 
 // ------------------------------------------------------------ RoIPool
@@ -627,7 +724,7 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     const int S = (ph + 1) * (pw + 1), n = R * S * 4;
     const unsigned ncell = (unsigned)ncell_sz;
     hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale,
-                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo);
+                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo, ph + 1, pw + 1);
     TLOD_LAUNCH_CHECK();
     size_t cb = w.cub_bytes;
     TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s,
@@ -640,9 +737,9 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     TLOD_LAUNCH_CHECK();
     TLOD_HIP(hipMemsetAsync(w.acc, 0, ncell_sz * C * sizeof(float), s));
     const int nseg = div_up(n, 64);
-    hipLaunchKernelGGL(rbg_seg_gather_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
-                       w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell, w.acc,
-                       w.carry_head, w.carry_tail, w.flags);
+    hipLaunchKernelGGL(rbg_seg_gather_kernel<false>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256),
+                       0, s, w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell, w.acc,
+                       w.carry_head, w.carry_tail, w.flags, S, pw + 1, 0, 0);
     TLOD_LAUNCH_CHECK();
     hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
                        w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
@@ -669,6 +766,83 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
                      0, s, acc, C, H * W, bottom_grad);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+// ResNet RoI-head entry (see roi_align_avg_s2_fwd_kernel): the forward needs the
+// channels-last map (B*H*W*C floats), the backward the gather workspace without its
+// sample-gradient rows; one query covers both.
+extern "C" size_t tlod_roi_align_avg_s2_workspace_bytes(int B, int C, int H, int W, int R, int ph,
+                                                        int pw) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || R <= 0 || ph <= 0 || pw <= 0) return 0;
+  Carve cv(nullptr, 0);
+  RbgWs w;
+  return std::max(carve_rbg(cv, w, B, C, H, W, R, ph, pw, true),
+                  align_up((size_t)B * H * W * C * sizeof(float), 256));
+}
+
+extern "C" int tlod_roi_align_avg_s2_nhwc_fwd_f32(const float* feat, int B, int C, int H, int W,
+                                                  const float* rois, int R, int ph, int pw,
+                                                  float scale, float* out, void* ws,
+                                                  size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0, "bad shape");
+  TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
+  if (R == 0) return kOk;
+  if (ws == nullptr || ws_bytes < (size_t)B * H * W * C * sizeof(float)) {
+    set_error("tlod_roi_align_avg_s2_nhwc_fwd_f32: workspace too small");
+    return kWorkspace;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  float* fn = static_cast<float*>(ws);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256), 0,
+                     s, feat, C, H * W, fn);
+  TLOD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(roi_align_avg_s2_fwd_kernel, dim3(R, div_up(C, 256)), dim3(256), 0, s, fn,
+                     scale, C, H, W, ph, pw, rois, out);
+  TLOD_LAUNCH_CHECK();
+  return kOk;
+}
+
+extern "C" int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, int C, int H,
+                                                  int W, const float* rois, int R, int ph, int pw,
+                                                  float scale, float* bottom_grad, void* ws,
+                                                  size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(B > 0 && C > 0 && H >= 2 && W >= 2 && R >= 0, "bad shape");
+  TLOD_CHECK_ARG(ph >= 1 && pw >= 1 && ph <= 7 && pw <= 7, "fused RoIAlignAvg supports 1..7 bins");
+  TLOD_CHECK_ARG((size_t)B * H * W < (1u << 31), "feature map too large");
+  if (R == 0) return kOk;
+  if (ws == nullptr || ws_bytes < tlod_roi_align_avg_s2_workspace_bytes(B, C, H, W, R, ph, pw)) {
+    set_error("tlod_roi_align_avg_s2_nhwc_bwd_f32: workspace too small");
+    return kWorkspace;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  Carve cv(ws, ws_bytes);
+  RbgWs w;
+  carve_rbg(cv, w, B, C, H, W, R, ph, pw, true);
+  const int S = (ph + 1) * (pw + 1), n = R * S * 4;
+  const int QH = (ph + 1) / 2, QW = (pw + 1) / 2;
+  const unsigned ncell = (unsigned)((size_t)B * H * W);
+  hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale, H,
+                     W, ph, pw, ncell, w.keys, w.vals, w.geo, 2 * QH, 2 * QW);
+  TLOD_LAUNCH_CHECK();
+  size_t cb = w.cub_bytes;
+  TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s, n,
+                                              0, rbg_bits(ncell), s));
+  hipLaunchKernelGGL(rbg_start_kernel, dim3(div_up((int)ncell + 1, 256)), dim3(256), 0, s, w.keys_s,
+                     n, ncell, w.start);
+  TLOD_LAUNCH_CHECK();
+  TLOD_HIP(hipMemsetAsync(w.acc, 0, (size_t)ncell * C * sizeof(float), s));
+  const int nseg = div_up(n, 64);
+  hipLaunchKernelGGL(rbg_seg_gather_kernel<true>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0,
+                     s, w.start, w.keys_s, w.vals_s, w.geo, top_grad, C, (int)ncell, w.acc,
+                     w.carry_head, w.carry_tail, w.flags, S, pw + 1, QH, QW);
+  TLOD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
+                     w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
+  TLOD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
+                     0, s, w.acc, C, H * W, bottom_grad);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }

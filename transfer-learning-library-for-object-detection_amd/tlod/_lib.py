@@ -51,6 +51,12 @@ SIGNATURES = {
                                                                  c_int, c_int]),
     "tlod_roi_align_avg_bwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
                                            c_float, P, P, c_size_t, P]),
+    "tlod_roi_align_avg_s2_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
+                                                         c_int]),
+    "tlod_roi_align_avg_s2_nhwc_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int,
+                                                   c_int, c_float, P, P, c_size_t, P]),
+    "tlod_roi_align_avg_s2_nhwc_bwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int,
+                                                   c_int, c_float, P, P, c_size_t, P]),
     "tlod_roi_pool_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,
                                       c_float, P, P, P]),
     "tlod_roi_pool_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),

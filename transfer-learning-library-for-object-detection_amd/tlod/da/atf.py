@@ -259,3 +259,4 @@ class resnet(_fasterRCNN):
 
     train = _daf_resnet.train
     _head_to_tail = _daf_resnet._head_to_tail
+    _pool = _daf_resnet._pool

@@ -339,6 +339,11 @@ class resnet(_fasterRCNN):
             set_bn_eval(self.RCNN_top)
         return self
 
+    def _pool(self, feat, rois):
+        # pool5 feeds only RCNN_top: the head entry (bins (2i, 2j), channels-last)
+        from ..detector.resnet import resnet_pool
+        return resnet_pool(self, feat, rois, _fasterRCNN._pool)
+
     def _head_to_tail(self, pool5):
         # RCNN_top(pool5).mean(3).mean(2) (resnet.py:286-288); the head runs channels-last
         return self.RCNN_top(pool5).mean(2).mean(1)

@@ -168,5 +168,9 @@ class resnet(_fasterRCNN):
             set_bn_eval(self.RCNN_top)
         return self
 
+    def _pool(self, feat, rois):
+        from .resnet import resnet_pool
+        return resnet_pool(self, feat, rois, _fasterRCNN._pool)
+
     def _head_to_tail(self, pool5):
         return self.RCNN_top(pool5).mean(2).mean(1)

@@ -18,12 +18,14 @@ in eval mode (:249-284).  Execution:
     would fill 16 of the 256 pixel slots of a conv tile.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
+from ..config import cfg
 from .. import conv as conv_mod
 from ..conv import ConvBNFunction, ShortcutLink
 from ..linear import LinearActFunction, LinearFunction, linear_math
@@ -186,9 +188,10 @@ class Bottleneck(nn.Module):
         return LinearActFunction.apply(xm.contiguous(), wm * scale[:, None], shift, residual,
                                        relu, m)
 
-    def forward_nhwc(self, x):
-        """x: (R, H, W, C) channels-last (the layer4 RoI head)."""
-        if self.stride == 2:
+    def forward_nhwc(self, x, subsampled=False):
+        """x: (R, H, W, C) channels-last (the layer4 RoI head); subsampled: x is already the
+        stride-2 subsample (the head entry, HeadEntry)."""
+        if self.stride == 2 and not subsampled:
             x = x[:, ::2, ::2, :]
         R, H, W, C = x.shape
         xm = x.reshape(R * H * W, C)
@@ -229,13 +232,42 @@ class ResNetBase(nn.Sequential):
         return x
 
 
+class HeadEntry:
+    """pool5 as RCNN_top reads it: the channels-last bins (2i, 2j) of RoIAlignAvg (R, QH, QW,
+    C) — layer4's first bottleneck subsamples by 2, so the rest of the 7 x 7 map is never
+    read (tlod.roi_align.roi_align_avg_s2_nhwc).  Returned by the ResNet models' _pool,
+    consumed only by their _head_to_tail."""
+
+    __slots__ = ("x",)
+
+    def __init__(self, x):
+        self.x = x
+
+
+def resnet_pool(model, feat, rois, base_pool):
+    """The ResNet detectors' _pool: the head entry for RoIAlignAvg (POOLING_MODE 'align'),
+    else the generic pooling (base_pool: the base class's _pool)."""
+    ra = model.RCNN_roi_align
+    first = model.RCNN_top[0][0]
+    if (cfg.POOLING_MODE == "align" and ra.aligned_height <= 7 and ra.aligned_width <= 7
+            and first.stride == 2 and os.environ.get("TLOD_ROI_HEAD_ENTRY", "1") != "0"):
+        from ..roi_align import roi_align_avg_s2_nhwc
+        return HeadEntry(roi_align_avg_s2_nhwc(feat, rois, ra.aligned_height, ra.aligned_width,
+                                               ra.spatial_scale))
+    return base_pool(model, feat, rois)
+
+
 class ResNetTop(nn.Sequential):
-    """RCNN_top = Sequential(layer4); forward(pool5 NCHW) -> channels-last features."""
+    """RCNN_top = Sequential(layer4); forward(pool5 NCHW, or the HeadEntry) -> channels-last
+    features."""
 
     def forward(self, pool5):
-        x = pool5.permute(0, 2, 3, 1)
-        for block in self[0]:
-            x = block.forward_nhwc(x)
+        if isinstance(pool5, HeadEntry):
+            x, sub = pool5.x, True
+        else:
+            x, sub = pool5.permute(0, 2, 3, 1), False
+        for i, block in enumerate(self[0]):
+            x = block.forward_nhwc(x, subsampled=sub and i == 0)
         return x
 
 

@@ -80,6 +80,53 @@ class RoIAlignAvgFunction(torch.autograd.Function):
         return grad_in, None, None, None, None
 
 
+class RoIAlignAvgS2Function(torch.autograd.Function):
+    """The ResNet RoI head's entry: RoIAlignAvg bins (2i, 2j), channels-last (R, QH, QW, C)
+    (tlod_roi_align_avg_s2_nhwc_*_f32) — RCNN_top = layer4 subsamples pool5 by 2 in its first
+    bottleneck (lib/DAF/resnet.py:64-102), so the other bins, the 7 x 7 map and its
+    channels-last permute are never needed.  Equal bit for bit to
+    RoIAlignAvgFunction(...).permute(0, 2, 3, 1)[:, ::2, ::2, :] and its gradient."""
+
+    @staticmethod
+    def forward(ctx, features, rois, pooled_height, pooled_width, spatial_scale):
+        _lib.require_cuda(features, rois)
+        feat = features.contiguous()
+        rois_c = rois.contiguous().float()
+        B, C, H, W = feat.shape
+        R = rois_c.shape[0]
+        ph, pw, sc = int(pooled_height), int(pooled_width), float(spatial_scale)
+        out = torch.empty((R, (ph + 1) // 2, (pw + 1) // 2, C), dtype=feat.dtype,
+                          device=feat.device)
+        L = _lib.lib()
+        ws = _lib.workspace(L.tlod_roi_align_avg_s2_workspace_bytes(B, C, H, W, max(R, 1), ph, pw),
+                            feat.device, "roi_align_s2")
+        _lib.check(L.tlod_roi_align_avg_s2_nhwc_fwd_f32(
+            _lib.ptr(feat), B, C, H, W, _lib.ptr(rois_c), R, ph, pw, sc, _lib.ptr(out),
+            _lib.ptr(ws), ws.numel(), _lib.stream_of(feat)), "roi_align_avg_s2_nhwc_fwd")
+        ctx.save_for_backward(rois_c)
+        ctx.meta = (B, C, H, W, ph, pw, sc)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (rois_c,) = ctx.saved_tensors
+        B, C, H, W, ph, pw, sc = ctx.meta
+        g = grad_output.contiguous()
+        R = rois_c.shape[0]
+        grad_in = torch.zeros((B, C, H, W), dtype=g.dtype, device=g.device)
+        L = _lib.lib()
+        ws = _lib.workspace(L.tlod_roi_align_avg_s2_workspace_bytes(B, C, H, W, max(R, 1), ph, pw),
+                            g.device, "roi_align_s2")
+        _lib.check(L.tlod_roi_align_avg_s2_nhwc_bwd_f32(
+            _lib.ptr(g), B, C, H, W, _lib.ptr(rois_c), R, ph, pw, sc, _lib.ptr(grad_in),
+            _lib.ptr(ws), ws.numel(), _lib.stream_of(g)), "roi_align_avg_s2_nhwc_bwd")
+        return grad_in, None, None, None, None
+
+
+def roi_align_avg_s2_nhwc(features, rois, pooled_height, pooled_width, spatial_scale):
+    return RoIAlignAvgS2Function.apply(features, rois, pooled_height, pooled_width, spatial_scale)
+
+
 class RoIAlign(Module):
     def __init__(self, aligned_height, aligned_width, spatial_scale):
         super().__init__()
