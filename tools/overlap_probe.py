@@ -9,7 +9,12 @@ Buckets are cut as tlod.dist.GradBucketReducer cuts them after its first-step re
 stream.  The exposed communication at a per-GPU bus bandwidth BW is
   max(0, end of the last bucket's all-reduce - end of backward)
 and the predicted step = measured 1-GPU step + exposed time.
-usage: python tools/overlap_probe.py [--steps 5] [--bucket-mb 32]"""
+With --contend, the same steps run again with an RCCL stand-in launched on a side stream
+when fc6's weight gradient (the 392 MB bucket) lands: tools/probe/libstreamer.so, a few
+one-wave workgroups streaming a buffer through HBM (a ring all-reduce's kernels hold a few
+dozen CUs and move ~2 (n-1)/n x B through HBM for a B-byte bucket), so the backward's
+slowdown under that contention is measured instead of assumed zero.
+usage: python tools/overlap_probe.py [--steps 5] [--bucket-mb 32] [--contend]"""
 import argparse
 import json
 import os
@@ -29,6 +34,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--contend", action="store_true")
+    ap.add_argument("--contend-wgs", type=int, default=32)
+    ap.add_argument("--contend-mb", type=float, default=686.0)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model = build_model("daf", dev, "vgg16")
@@ -95,7 +103,71 @@ def main():
            "backward_left_after_bucket_ms": [round(bwd - t, 3) for _, t in buckets],
            "bucket_mb": [round(b / 2**20, 1) for b, _ in buckets],
            "ranks": n, "prediction": pred}
+    if a.contend:
+        out["contention"] = contend(a, model, opt, data, marks, r)
     print(json.dumps(out))
+
+
+def contend(a, model, opt, data, marks, base):
+    """Backward time with the RCCL stand-in streaming from fc6's gradient landing onward."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probe", "libstreamer.so"))
+    lib.streamer_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    nbytes = int(a.contend_mb * 2**20) // 16 * 16
+    src = torch.empty(nbytes // 4, device="cuda")
+    dst = torch.empty_like(src)
+    side = torch.cuda.Stream()
+
+    def launch():
+        return lib.streamer_launch(src.data_ptr(), dst.data_ptr(), nbytes, a.contend_wgs, 1,
+                                   side.cuda_stream)
+    # standalone duration of the stand-in
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(side):
+        launch()
+        torch.cuda.synchronize()
+        s0.record(side)
+        launch()
+        s1.record(side)
+    torch.cuda.synchronize()
+    alone = s0.elapsed_time(s1)
+    fc6 = max((p for p in model.parameters() if p.requires_grad), key=lambda p: p.numel())
+    hook_state = {"on": False}
+
+    def on_grad(p):
+        if hook_state["on"] and p is fc6:
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            launch()
+            hook_state["on"] = False
+    from tlod.grads import arena_of
+    arena_of(fc6).listeners.append(on_grad)
+    runs = []
+    for _ in range(a.steps):
+        opt.zero_grad(set_to_none=True)
+        e0, e_fwd, e_bwd, e_end = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+        batch = data.next()
+        e0.record()
+        out = model(*batch)
+        loss = model.total_loss(out, 0.1)
+        e_fwd.record()
+        hook_state["on"] = True
+        loss.backward()
+        e_bwd.record()
+        torch.cuda.current_stream().wait_stream(side)
+        opt.step(grad_scale=1.0)
+        e_end.record()
+        torch.cuda.synchronize()
+        runs.append((e_fwd.elapsed_time(e_bwd), e0.elapsed_time(e_end)))
+    bwd, step = sorted(runs)[len(runs) // 2]
+    return {"standin_wgs": a.contend_wgs, "standin_bytes_moved_mb": round(2 * nbytes / 2**20, 1),
+            "standin_alone_ms": round(alone, 3),
+            "standin_alone_GBps": round(2 * nbytes / alone / 1e6, 1),
+            "bwd_ms": round(bwd, 3), "bwd_ms_alone": round(base["bwd_ms"], 3),
+            "bwd_slowdown_ms": round(bwd - base["bwd_ms"], 3),
+            "step_ms_with_standin_joined": round(step, 3)}
 
 
 if __name__ == "__main__":
