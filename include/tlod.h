@@ -52,6 +52,10 @@ enum tlod_status {
 
 int tlod_abi_version(void);
 const char* tlod_last_error(void);
+/* CUs the split-K / round planners leave out (default 0, or env TLOD_CU_RESERVE): set by the
+ * data-parallel reducer (tlod/dist.py) while its all-reduces run beside the backward, whose
+ * kernels then hold a few CUs; process-wide, read at every launch.  0 <= cus <= 1024. */
+int tlod_set_cu_reserve(int cus);
 
 /* ------------------------------------------------------------------ NMS
  * Replaces: nms_cuda(THCudaIntTensor* keep_out, THCudaTensor* boxes, THCudaIntTensor*

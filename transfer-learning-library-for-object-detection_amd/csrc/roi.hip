@@ -258,16 +258,12 @@ __global__ void __launch_bounds__(kNhwcThreads) roi_align_avg_bwd_nhwc_kernel(
 // sg 73 MB written and read once per tap (~290 MB, mostly L2 / Infinity-Cache hits),
 // bottom_grad 11 MB read + written.
 
-// (sy_lim, sx_lim: samples at rows >= sy_lim or columns >= sx_lim feed no output bin — the
-// stride-2 head entry's bins (2i, 2j) leave the last sample row / column of an even bin
-// count uncovered — and get the sentinel key like samples outside the map)
 __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__ rois, int R,
                                                        float scale, int H, int W, int ph, int pw,
                                                        unsigned ncell,
                                                        unsigned* __restrict__ keys,
                                                        unsigned* __restrict__ vals,
-                                                       float2* __restrict__ geo, int sy_lim,
-                                                       int sx_lim) {
+                                                       float2* __restrict__ geo) {
   const int ah = ph + 1, aw = pw + 1, S = ah * aw;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R * S) return;
@@ -278,7 +274,7 @@ __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__
   bool vy, vx;
   align_axis(ro[2] * scale, ro[4] * scale, ah, sy, H, &y, &hr, &vy);
   align_axis(ro[1] * scale, ro[3] * scale, aw, sx, W, &x, &wr, &vx);
-  const bool ok = vy && vx && sy < sy_lim && sx < sx_lim;
+  const bool ok = vy && vx;
   const unsigned c00 = (unsigned)(((int)ro[0] * H + y) * W + x);
   geo[i] = make_float2(hr, wr);
 #pragma unroll
@@ -388,9 +384,13 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
     for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
       const unsigned vu = __builtin_amdgcn_readlane(vl, min(j + u, jn - 1));
       if constexpr (S2) {
+        // (a sample past the last selected bin — the last row / column of an even bin count —
+        // keeps its taps with value 0, so the taps and their segments are those of the
+        // zero-padded 7 x 7 backward: the same sums in the same association)
         const int row = (int)(vu >> 2), r = row / S, smp = row - r * S;
-        const int trow = (r * QH + (smp / aw >> 1)) * QW + ((smp % aw) >> 1);
-        sv[u] = cok ? sg[(size_t)trow * C + c] * 0.25f : 0.f;  // = top / 4.f exactly
+        const int hy = smp / aw >> 1, hx = (smp % aw) >> 1;
+        const bool cov = hy < QH && hx < QW;
+        sv[u] = cok && cov ? sg[((size_t)(r * QH + hy) * QW + hx) * C + c] * 0.25f : 0.f;  // = top / 4.f
       } else {
         sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
       }
@@ -520,7 +520,8 @@ __global__ void __launch_bounds__(256) nhwc_add_to_nchw_kernel(const float* __re
 // permute to channels-last or the strided subsample copy is materialised.  Values are the
 // fused NCHW kernel's bit for bit (same samples, same average order).  The bins (2i, 2j)
 // cover disjoint 2 x 2 sample blocks, so the backward gives each sample its bin's top / 4
-// with no sample-gradient pass (rbg_seg_gather_kernel<true>).
+// with no sample-gradient pass (rbg_seg_gather_kernel<true>); the backward is therefore equal
+// bit for bit to the 7 x 7 backward of a top gradient that is zero off the selected bins.
 
 // out (B, HW, C) = in (B, C, HW): 64 x 64 tiles through LDS
 __global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ in, int C,
@@ -724,7 +725,7 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     const int S = (ph + 1) * (pw + 1), n = R * S * 4;
     const unsigned ncell = (unsigned)ncell_sz;
     hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale,
-                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo, ph + 1, pw + 1);
+                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo);
     TLOD_LAUNCH_CHECK();
     size_t cb = w.cub_bytes;
     TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s,
@@ -824,7 +825,7 @@ extern "C" int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, 
   const int QH = (ph + 1) / 2, QW = (pw + 1) / 2;
   const unsigned ncell = (unsigned)((size_t)B * H * W);
   hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale, H,
-                     W, ph, pw, ncell, w.keys, w.vals, w.geo, 2 * QH, 2 * QW);
+                     W, ph, pw, ncell, w.keys, w.vals, w.geo);
   TLOD_LAUNCH_CHECK();
   size_t cb = w.cub_bytes;
   TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s, n,

@@ -569,7 +569,7 @@ static WgwsPlan wgws_plan(int N, int Cin, int H, int W, int Cout) {
   const int chunks = N * div_up(H, TH) * div_up(W, TW);
   // cost: rounds x chunks per split x chunk time + the slab round trip (sp writes + sp
   // reads of the partial tiles); one resident workgroup per CU (139 KB LDS)
-  const int slots = 256;
+  const int slots = cached_slots((const void*)wgrad_ws_kernel, NT, LDS_BYTES);
   const double chunk_s = 1728.0 * 16.0 / 4.0 / 2.1e9 / 0.75;  // 1728 16x16x32 MFMAs per chunk
   const double tile_bytes = (double)TILE_FLOATS * 4.0;
   int best = 1;

@@ -38,6 +38,7 @@ class RcnnCfg(ctypes.Structure):
 SIGNATURES = {
     "tlod_abi_version": (c_int, []),
     "tlod_last_error": (ctypes.c_char_p, []),
+    "tlod_set_cu_reserve": (c_int, [c_int]),
     "tlod_nms_workspace_bytes": (c_size_t, [c_int]),
     "tlod_nms_f32": (c_int, [P, c_int, c_int, c_float, c_int, P, P, P, c_size_t, P]),
     "tlod_roi_align_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int,

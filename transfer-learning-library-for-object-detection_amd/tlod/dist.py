@@ -50,6 +50,11 @@ def init_from_env(backend=None):
     return rank, world
 
 
+def _set_cu_reserve(n):
+    from . import _lib
+    _lib.check(_lib.lib().tlod_set_cu_reserve(int(n)), "set_cu_reserve")
+
+
 class GradBucketReducer:
     def __init__(self, model, bucket_mb=32.0, group=None, relayout=True, arena=None):
         self.group = group
@@ -75,6 +80,17 @@ class GradBucketReducer:
         self.cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         self.relayout_pending = relayout
         self.seen = []  # rank-local gradient-ready order of this step (parameter indices)
+        # CUs the kernels' round planners leave free while the step's all-reduces run beside
+        # the backward (tlod_set_cu_reserve): RCCL's kernels hold a few CUs, and a grid
+        # planned for exactly one round of all 256 would run a second round for the few
+        # workgroups left over.  With a 32-workgroup HBM-streaming stand-in launched at fc6's
+        # gradient, the DAF-VGG16 backward took +2.8 ms with no reserve and +0.8 ms with 32
+        # (profiles/r05/overlap_contention.json); a reserve costs ~8% on the
+        # kernels it covers when nothing competes, so it is on only while collectives are in
+        # flight, and only for RCCL (gloo reduces on the host).
+        backend = dist.get_backend(group)
+        self.cu_reserve = int(os.environ.get("TLOD_DIST_CU_RESERVE",
+                                             "32" if backend == "nccl" else "0"))
         self._build_buckets()
         arena.listeners.append(self._on_grad)
 
@@ -122,6 +138,8 @@ class GradBucketReducer:
             b = self.buckets[self.next]
             if b["ready"] != len(b["params"]) + (self.next == len(self.buckets) - 1):
                 return
+            if self.next == 0 and self.cu_reserve:
+                _set_cu_reserve(self.cu_reserve)
             b["work"] = dist.all_reduce(self._flat(b), op=dist.ReduceOp.SUM, group=self.group,
                                         async_op=True)
             self.next += 1
@@ -171,6 +189,8 @@ class GradBucketReducer:
         self._launch_ready_prefix()
         for b in self.buckets:
             b["work"].wait()
+        if self.cu_reserve:
+            _set_cu_reserve(0)
         for p in unmarked:
             p.grad = a.view(p)
         seen = self.seen
