@@ -68,6 +68,22 @@ def main():
         tc.conv_dgrad(g, w, wd=wd, math=m)
         torch.cuda.current_stream().wait_stream(side)
     out["bwd_pair_ms"] = timeit(pair, a.iters)
+    # the same with dgrad on a high-priority stream: the dispatcher places every dgrad
+    # workgroup before any wgrad one, wgrad filling dgrad's last partial round
+    hi = torch.cuda.Stream(priority=-1)
+
+    def pair_prio():
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(hi):
+            hi.wait_event(ev)
+            tc.conv_dgrad(g, w, wd=wd, math=m)
+        with torch.cuda.stream(side):
+            side.wait_event(ev)
+            tc.conv_wgrad(g, x, 3, out=dw, math=m)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.current_stream().wait_stream(hi)
+    out["bwd_pair_prio_ms"] = timeit(pair_prio, a.iters)
     for k in ("fwd", "dgrad", "wgrad"):
         out[k + "_tflops"] = flop / (out[k + "_ms"] * 1e-3) / 1e12
     bwd = out["dgrad_ms"] + out["wgrad_ms"]
