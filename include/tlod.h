@@ -462,6 +462,38 @@ int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float grad_sca
                       float momentum, float clip_norm, float* partials, float* norm_scale,
                       tlod_stream_t stream);
 
+/* The same step with the split-bf16 weight packs of 3x3 conv weights written by the update
+ * itself (no per-weight tlod_conv_pack_bs launches before the next forward / backward).
+ * chunks[0, n_update) are updated as above; chunks[n_update, n_chunks) only enter the
+ * gradient norm: their parameters are the 3x3 weights the tiles update.  A tile is 32 output
+ * x 32 input channels x 9 taps of one (cout, cin, 3, 3) weight (o0, i0: its first output /
+ * input channel, multiples of 32); it applies the SGD update to its elements and stores the
+ * new weights into each non-NULL pack — pack_fwd: the tlod_conv_pack_bs(dgrad = 0) layout,
+ * pack_dgrad: dgrad = 1, pack_dgrad_scaled: tlod_conv_pack_bs_ex(scale, dgrad = 1) — bit
+ * for bit what those functions would produce from the updated weight.  The packs must have
+ * been made once by those functions (the tiles do not write their zero padding).  active as
+ * for chunks (the tile, weight and packs are left untouched). */
+typedef struct tlod_sgd_pack_tile {
+  float* param;
+  const float* grad;
+  float* momentum_buf;
+  const float* active;
+  unsigned short* pack_fwd;
+  unsigned short* pack_dgrad;
+  unsigned short* pack_dgrad_scaled;
+  const float* scale;
+  float lr;
+  float weight_decay;
+  int cout, cin;
+  int o0, i0;
+  int reserved[2];
+} tlod_sgd_pack_tile;
+
+int tlod_sgd_clip_pack_f32(const tlod_sgd_chunk* chunks, int n_chunks, int n_update,
+                           const tlod_sgd_pack_tile* tiles, int n_tiles, float grad_scale,
+                           float momentum, float clip_norm, float* partials, float* norm_scale,
+                           tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ Input blob
  * Replaces: the data layer's per-image host chain — scipy imread (RGB) -> BGR -> flip
  *   (lib/roi_data_layer/minibatch.py:62-82) -> astype(float32) -= PIXEL_MEANS ->

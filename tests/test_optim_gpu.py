@@ -55,3 +55,63 @@ def test_params_without_grad_are_skipped():
     for p, b in zip(unused.parameters(), before):
         assert torch.equal(p.detach(), b)
     assert all(p.grad is None for p in unused.parameters())
+
+
+@pytest.mark.parametrize("clip", [0.0, 10.0])
+def test_fused_pack_update(clip, monkeypatch):
+    """tlod_sgd_clip_pack_f32: the 3x3 weights a FusedSGDClip owns are updated by tiles that
+    also write their split-bf16 packs.  After every step the packs the convs will use (the
+    cached ones: no re-pack, PACK_GEN unchanged) are bit-identical to packs made from the
+    updated weights, and the weights match the chunk-only update (TLOD_SGD_PACK=0) — bit for
+    bit without clipping (with it the norm's partials are summed in another order).  Ragged
+    channel counts (tiles past the last channel), a BN-scaled input-gradient pack, Cin = 3."""
+    from tlod import conv
+    from tlod.optim import FusedSGDClip
+    shapes = [(40, 24), (64, 64), (80, 36), (256, 128), (16, 3), (33, 65)]
+    g = torch.Generator(device="cuda").manual_seed(1)
+
+    def params():
+        torch.manual_seed(3)
+        ws = [torch.nn.Parameter(torch.randn(co, ci, 3, 3, device="cuda") * 0.05) for co, ci in shapes]
+        return ws + [torch.nn.Parameter(torch.randn(40, device="cuda"))]
+
+    pa, pb = params(), params()
+    scale = torch.rand(80, device="cuda") + 0.5
+    groups = lambda ps: [{"params": ps[:-1], "lr": 0.01, "weight_decay": 5e-4},
+                         {"params": ps[-1:], "lr": 0.02, "weight_decay": 0.0}]
+    monkeypatch.setenv("TLOD_SGD_PACK", "1")
+    fo = FusedSGDClip(groups(pa), momentum=0.9, clip_norm=clip)
+    monkeypatch.setenv("TLOD_SGD_PACK", "0")
+    ro = FusedSGDClip(groups(pb), momentum=0.9, clip_norm=clip)
+    assert all(getattr(w, "_tlod_pack_owner", False) for w in pa[:-1])
+    assert not any(getattr(w, "_tlod_pack_owner", False) for w in pb)
+
+    def packs():
+        out = []
+        for w in pa[:-1]:
+            out += [conv.pack_bs(w, False), conv.pack_bs(w, True)]
+        return out + [conv.pack_bs(pa[2], True, scale)]
+    first = packs()
+    gen = conv.PACK_GEN[0]
+    for step in range(3):
+        rs = [torch.randn(p.shape, device="cuda", generator=g) for p in pa]
+        for ps, opt in ((pa, fo), (pb, ro)):
+            opt.zero_grad()
+            sum((p * r).sum() for p, r in zip(ps, rs)).backward()
+            opt.step()
+        for a, b in zip(pa, pb):
+            if clip == 0:
+                assert torch.equal(a.detach(), b.detach())
+            else:
+                torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-7)
+        now = packs()
+        assert conv.PACK_GEN[0] == gen and all(x is y for x, y in zip(now, first))
+        fresh = []
+        for w in pa[:-1]:
+            fresh += [conv._pack_bs(w, False), conv._pack_bs(w, True)]
+        fresh.append(conv._pack_bs(pa[2], True, scale))
+        for i, (x, y) in enumerate(zip(now, fresh)):
+            assert torch.equal(x, y), (step, i)
+    # a trainable weight no fused optimizer owns is packed afresh on every use
+    w = torch.nn.Parameter(torch.randn(8, 8, 3, 3, device="cuda"))
+    assert conv.pack_bs(w, False) is not conv.pack_bs(w, False)

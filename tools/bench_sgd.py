@@ -1,33 +1,57 @@
-"""Microbenchmark: the fused clip + SGD step (tlod_sgd_clip_f32) over DAF-VGG16's trainable
-parameter shapes (~137 M floats), HIP events around optimizer.step()."""
+"""Optimizer step microbench: the fused clip + SGD over DAF-VGG16-shaped trainable parameters,
+with the 3x3 weight packs either written by the update's tiles (TLOD_SGD_PACK=1) or made by
+tlod_conv_pack_bs launches before the next use (0: one fwd + one dgrad pack per weight, as
+the step does).  Prints JSON: ms per step (step + packs) and the kernel split."""
+import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "transfer-learning-library-for-object-detection_amd"))
-import torch  # noqa: E402
+import torch
 
-from tlod.detector.train import build_model, make_optimizer  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..",
+                                "transfer-learning-library-for-object-detection_amd"))
 
-dev = torch.device("cuda", 0)
-model = build_model("daf", dev, "vgg16")
-opt = make_optimizer(model, 2e-3, clip=10.0)
-n = 0
-for p in opt.params:
-    g = opt.arena.view(p) if opt.arena is not None else torch.empty_like(p)
-    g.normal_()
-    p.grad = g
-    n += p.numel()
-for _ in range(3):
-    opt.step()
-s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-torch.cuda.synchronize()
-s.record()
-it = 20
-for _ in range(it):
-    opt.step()
-e.record()
-torch.cuda.synchronize()
-ms = s.elapsed_time(e) / it
-print(f"params {n / 1e6:.1f} M, step {ms:.3f} ms, {24 * n / (ms * 1e-3) / 1e12:.2f} TB/s "
-      f"(6 x 4 B per parameter: g read twice, p and buf read + written)")
+
+def main():
+    from tlod import conv
+    from tlod.optim import FusedSGDClip
+    torch.manual_seed(0)
+    convs = [(256, 128), (256, 256), (256, 256), (512, 256), (512, 512), (512, 512),
+             (512, 512), (512, 512), (512, 512), (512, 512)]
+    ws = [torch.nn.Parameter(torch.randn(co, ci, 3, 3, device="cuda") * 0.01) for co, ci in convs]
+    fcs = [torch.nn.Parameter(torch.randn(4096, 25088, device="cuda") * 0.001),
+           torch.nn.Parameter(torch.randn(4096, 4096, device="cuda") * 0.01)]
+    bs = [torch.nn.Parameter(torch.zeros(co, device="cuda")) for co, _ in convs]
+    params = ws + fcs + bs
+    fused = os.environ.get("TLOD_SGD_PACK", "1") != "0"
+    opt = FusedSGDClip([{"params": ws + fcs, "lr": 1e-3, "weight_decay": 5e-4},
+                        {"params": bs, "lr": 2e-3, "weight_decay": 0.0}], clip_norm=10.0)
+    for p in params:
+        p.grad = torch.randn_like(p) * 1e-3
+
+    def packs():
+        for i, w in enumerate(ws):
+            conv.pack_bs(w, False)
+            if i:
+                conv.pack_bs(w, True)
+
+    packs()
+    for _ in range(3):
+        opt.step()
+        packs()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 20
+    e0.record()
+    for _ in range(n):
+        opt.step()
+        packs()
+    e1.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"fused_packs": fused, "ms_per_step": round(e0.elapsed_time(e1) / n, 4),
+                      "params": sum(p.numel() for p in params),
+                      "conv3x3_params": sum(w.numel() for w in ws)}))
+
+
+if __name__ == "__main__":
+    main()

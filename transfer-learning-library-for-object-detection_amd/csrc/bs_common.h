@@ -6,6 +6,10 @@
 
 namespace tlod {
 
+// Packed 3x3 weight row (pack_bs_kernel in conv.hip, and the fused SGD in optim.hip that
+// keeps the packs current): per 8-channel chunk 10 tap slots (9 + a zero pad) x 8 channels.
+constexpr int kBsKP = 80;
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // XCD-aware bijective remap: consecutive hardware ids round-robin over 8 XCDs; give

@@ -390,7 +390,7 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_kernel(
 // bf16 planes [pos][8 ch].  Weight rows use a 176-B pitch so the 16-lane ds_read_b128
 // groups are conflict-free; patch positions are 16 B apart (conflict-free as is).
 
-constexpr int kBsKP = 80;  // packed k per chunk: 10 taps (9 + zero pad) x 8 channels
+// kBsKP (bs_common.h): packed k per chunk, 10 taps (9 + zero pad) x 8 channels
 
 // Band tiles (narrow maps, W <= ~100): a tile is 512 consecutive flattened pixels
 // p = h*W + w (16 groups of 32, one per MFMA column block) instead of 16 rows x 32 columns,

@@ -94,6 +94,7 @@ SIGNATURES = {
                                     c_size_t, P]),
     "tlod_relu_bwd_bias_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, P]),
     "tlod_sgd_clip_f32": (c_int, [P, c_int, c_float, c_float, c_float, P, P, P]),
+    "tlod_sgd_clip_pack_f32": (c_int, [P, c_int, c_int, P, c_int, c_float, c_float, c_float, P, P, P]),
     "tlod_conv_fwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, P, c_size_t, P]),
     "tlod_relu_bwd_ex_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, P]),

@@ -156,22 +156,38 @@ def weights_updated():
     _EXTERNAL_WRITES[0] += 1
 
 
-def pack_bs(weight, dgrad):
-    """Pre-split bf16 planes of a 3x3 weight for the split-bf16 fwd (dgrad=0) / dgrad (1).
-    Frozen weights (requires_grad False: conv1/conv2 of VGG16, the fixed ResNet blocks) are
-    packed once per (storage, version), cached on the tensor itself — an in-place load bumps
-    the version, a write that bypasses it (the data-parallel broadcast) calls
-    weights_updated().  Trainable weights are repacked every call (the fused SGD
-    writes them without a version bump; packing all of them in one launch per step,
-    tried in round 4, was no faster).  One cached pack per tensor."""
-    if not weight.requires_grad:
-        cache = getattr(weight, "_tlod_packs", None)  # lives and dies with the tensor
-        key = (weight.data_ptr(), weight._version, bool(dgrad), _EXTERNAL_WRITES[0])
-        if cache is None or cache[0] != key:
-            cache = (key, _pack_bs(weight, dgrad))
-            weight._tlod_packs = cache
-        return cache[1]
-    return _pack_bs(weight, dgrad)
+# Generation of the set of packs that tlod.optim.FusedSGDClip keeps current: bumped when a
+# pack of a weight it owns is (re)made, so the optimizer rebuilds its tile table.
+PACK_GEN = [0]
+
+
+def pack_bs(weight, dgrad, scale=None):
+    """Pre-split bf16 planes of a 3x3 weight for the split-bf16 fwd (dgrad=0) / dgrad (1);
+    scale (Cout, optional): of weight[co] * scale[co] (a frozen BatchNorm's scale after the
+    conv).  Cached on the tensor per (dgrad, scale) for frozen weights (requires_grad False:
+    conv1/conv2 of VGG16, the fixed ResNet blocks) and for weights a FusedSGDClip owns
+    (`_tlod_pack_owner`: its update writes the new packs in the same kernel,
+    tlod_sgd_clip_pack_f32); valid per (storage, version, external writes) — an in-place load
+    bumps the version, a write that bypasses it (the data-parallel broadcast) calls
+    weights_updated().  Other trainable weights are repacked every call."""
+    owned = weight.requires_grad and getattr(weight, "_tlod_pack_owner", False)
+    if weight.requires_grad and (not owned or (scale is not None and not dgrad)):
+        return _pack_bs(weight, dgrad, scale)  # (the fused update keeps no scaled fwd pack)
+    packs = getattr(weight, "_tlod_packs", None)  # lives and dies with the tensor
+    if packs is None:
+        packs = weight._tlod_packs = {}
+    vkey = (bool(dgrad), None if scale is None else (scale.data_ptr(), scale._version))
+    key = (weight.data_ptr(), weight._version, _EXTERNAL_WRITES[0])
+    hit = packs.get(vkey)
+    if hit is None or hit[0] != key:
+        if scale is not None:  # one scaled variant per weight (the fused update's tile has one)
+            for k in [k for k in packs if k[1] is not None]:
+                del packs[k]
+        hit = (key, _pack_bs(weight, dgrad, scale), scale)
+        packs[vkey] = hit
+        if owned:
+            PACK_GEN[0] += 1
+    return hit[1]
 
 
 def _pack_bs(weight, dgrad, scale=None):
@@ -303,7 +319,7 @@ def conv_dgrad(g, weight, wd=None, math=None, mask=None, residual=None, wscale=N
         return dx
     if wscale is not None:
         if _bs(KS, math) and not _gemm_conv(KS, math, Cin) and wd is None:
-            wd = _pack_bs(weight, True, wscale)
+            wd = pack_bs(weight, True, wscale)
         else:
             weight = weight.detach() * wscale.view(-1, 1, 1, 1)
             wd = None

@@ -6,6 +6,12 @@ by ``torch.optim.SGD(params, momentum=0.9)`` with the reference's param groups
 BIAS_DECAY; weights lr and WEIGHT_DECAY) — three launches, no host wait: the gradients
 live in the persistent arena (tlod.grads), so the descriptor table is built and uploaded
 once per (arena layout, set of parameters with a gradient, learning rates).
+
+3x3 conv weights are updated by tiles that also write their split-bf16 packs (the conv
+kernels' operand layouts, tlod_sgd_clip_pack_f32): the optimizer marks them as owned
+(`_tlod_pack_owner`), tlod.conv.pack_bs then caches their packs, and the next forward and
+backward use the packs this step wrote instead of re-packing every weight.  TLOD_SGD_PACK=0
+turns that off (every trainable 3x3 weight re-packed per use, as before).
 """
 import os
 
@@ -13,6 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from . import conv as _conv
 from .grads import GradArena, arena_of
 
 CHUNK = 65536
@@ -20,6 +27,31 @@ _DESC = np.dtype([("param", np.uint64), ("grad", np.uint64), ("buf", np.uint64),
                   ("count", np.int64), ("lr", np.float32), ("wd", np.float32),
                   ("active", np.uint64)])
 assert _DESC.itemsize == 48  # sizeof(tlod_sgd_chunk), include/tlod.h
+_TILE = np.dtype([("param", np.uint64), ("grad", np.uint64), ("buf", np.uint64),
+                  ("active", np.uint64), ("pack_fwd", np.uint64), ("pack_dgrad", np.uint64),
+                  ("pack_dgrad_scaled", np.uint64), ("scale", np.uint64), ("lr", np.float32),
+                  ("wd", np.float32), ("cout", np.int32), ("cin", np.int32), ("o0", np.int32),
+                  ("i0", np.int32), ("reserved", np.int32, 2)])
+assert _TILE.itemsize == 96  # sizeof(tlod_sgd_pack_tile), include/tlod.h
+TILE = 32  # channels per tile side (optim.hip kPT)
+
+
+def _packs_of(p):
+    """(fwd pack, dgrad pack, scaled dgrad pack, its scale) the fused update can keep
+    current, or None when the weight has none yet."""
+    packs = getattr(p, "_tlod_packs", None)
+    if not packs:
+        return None
+    pf = pd = pds = sc = None
+    for (dgrad, skey), (_, pk, scale) in packs.items():
+        if skey is None:
+            if dgrad:
+                pd = pk
+            else:
+                pf = pk
+        elif dgrad:
+            pds, sc = pk, scale
+    return (pf, pd, pds, sc) if (pf is not None or pd is not None or pds is not None) else None
 
 
 class FusedSGDClip:
@@ -33,6 +65,11 @@ class FusedSGDClip:
         self.params = [p for g in self.param_groups for p in g["params"]]
         for p in self.params:
             _lib.require_cuda(p)
+        self.fused_packs = os.environ.get("TLOD_SGD_PACK", "1") != "0"
+        if self.fused_packs:
+            for p in self.params:
+                if p.dim() == 4 and tuple(p.shape[2:]) == (3, 3):
+                    p._tlod_pack_owner = True
         dev = self.params[0].device
         self.bufs = [torch.zeros_like(p) for p in self.params]
         n_chunks = sum((p.numel() + CHUNK - 1) // CHUNK for p in self.params)
@@ -47,8 +84,6 @@ class FusedSGDClip:
         # descriptor tables per gradient-pointer set; with the arena the key is stable and
         # the (blocking, tiny) upload happens on the first step only
         self._tables = {}
-        self._key = None
-        self._n = 0
 
     def zero_grad(self, set_to_none=True):
         if set_to_none and self.arena is not None:
@@ -60,56 +95,73 @@ class FusedSGDClip:
             elif p.grad is not None:
                 p.grad.zero_()
 
-    def _chunk_table(self):
-        """Descriptor rows for every parameter that has a gradient (torch.optim.SGD skips
-        the others entirely: no weight decay, no momentum update)."""
-        grads = [p.grad for p in self.params]
-        a = self.arena
-        act = a.active if a is not None and a.active is not None else None
-        key = tuple(0 if g is None else g.data_ptr() for g in grads) + \
-            tuple(g["lr"] for g in self.param_groups) + (0 if act is None else act.data_ptr(),)
-        hit = self._tables.get(key)
-        if hit is not None:
-            self._n = hit[1]
-            return hit[0]
-        rows = []
-        idx = 0
-        for g in self.param_groups:
-            for p in g["params"]:
-                gr, buf = p.grad, self.bufs[idx]
-                if gr is None:
-                    idx += 1
-                    continue
-                assert gr.is_contiguous() and p.is_contiguous()
-                n = p.numel()
-                # data parallel: skipped on the device when no rank produced the gradient
-                ap = 0 if act is None else act.data_ptr() + 4 * a.index[p]
-                for off in range(0, n, CHUNK):
-                    rows.append((p.data_ptr() + 4 * off, gr.data_ptr() + 4 * off,
-                                 buf.data_ptr() + 4 * off, min(CHUNK, n - off), g["lr"],
-                                 g.get("weight_decay", 0.0), ap))
-                idx += 1
-        arr = np.array(rows, dtype=_DESC)
-        table = torch.empty(arr.nbytes, dtype=torch.uint8, device=self.partials.device)
+    def _upload(self, arr):
+        table = torch.empty(max(arr.nbytes, 1), dtype=torch.uint8, device=self.partials.device)
         if arr.nbytes:
             host = torch.empty(arr.nbytes, dtype=torch.uint8, pin_memory=True)
             host.numpy()[:] = arr.view(np.uint8)
             table.copy_(host)
+        return table
+
+    def _chunk_table(self):
+        """Descriptor rows for every parameter that has a gradient (torch.optim.SGD skips
+        the others entirely: no weight decay, no momentum update): (chunk table, tile table,
+        rows updated by chunks, rows, tiles).  The 3x3 weights with packs get tiles; their
+        chunk rows come last and only enter the gradient norm."""
+        grads = [p.grad for p in self.params]
+        a = self.arena
+        act = a.active if a is not None and a.active is not None else None
+        key = tuple(0 if g is None else g.data_ptr() for g in grads) + \
+            tuple(g["lr"] for g in self.param_groups) + \
+            (0 if act is None else act.data_ptr(), _conv.PACK_GEN[0] if self.fused_packs else 0)
+        hit = self._tables.get(key)
+        if hit is not None:
+            return hit
+        rows, norm_rows, tiles, keep = [], [], [], []
+        idx = 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                gr, buf = p.grad, self.bufs[idx]
+                idx += 1
+                if gr is None:
+                    continue
+                assert gr.is_contiguous() and p.is_contiguous()
+                n = p.numel()
+                lr, wd = g["lr"], g.get("weight_decay", 0.0)
+                # data parallel: skipped on the device when no rank produced the gradient
+                ap = 0 if act is None else act.data_ptr() + 4 * a.index[p]
+                packs = _packs_of(p) if self.fused_packs and getattr(p, "_tlod_pack_owner",
+                                                                     False) else None
+                dest = rows if packs is None else norm_rows
+                for off in range(0, n, CHUNK):
+                    dest.append((p.data_ptr() + 4 * off, gr.data_ptr() + 4 * off,
+                                 buf.data_ptr() + 4 * off, min(CHUNK, n - off), lr, wd, ap))
+                if packs is None:
+                    continue
+                keep.append(packs)  # the table holds their pointers
+                pf, pd, pds, sc = (0 if t is None else t.data_ptr() for t in packs)
+                cout, cin = p.shape[0], p.shape[1]
+                for o0 in range(0, cout, TILE):
+                    for i0 in range(0, cin, TILE):
+                        tiles.append((p.data_ptr(), gr.data_ptr(), buf.data_ptr(), ap, pf, pd,
+                                      pds, sc, lr, wd, cout, cin, o0, i0, (0, 0)))
+        chunks = self._upload(np.array(rows + norm_rows, dtype=_DESC))
+        tile_t = self._upload(np.array(tiles, dtype=_TILE))
         if len(self._tables) >= 8:
             self._tables.pop(next(iter(self._tables)))
-        self._tables[key] = (table, len(rows))
-        self._key, self._n = key, len(rows)
-        return table
+        hit = (chunks, tile_t, len(rows), len(rows) + len(norm_rows), len(tiles), keep)
+        self._tables[key] = hit
+        return hit
 
     @torch.no_grad()
     def step(self, grad_scale=1.0):
         """grad_scale: factor applied to every gradient as it is read (data parallel: 1/world
         of the all-reduced sums, tlod.dist.GradBucketReducer.grad_scale)."""
-        table = self._chunk_table()
-        if self._n == 0:
+        chunks, tiles, n_update, n, n_tiles, _ = self._chunk_table()
+        if n == 0:
             return self.norm_scale[0]
-        _lib.check(_lib.lib().tlod_sgd_clip_f32(
-            _lib.ptr(table), self._n, float(grad_scale), self.momentum, self.clip_norm,
-            _lib.ptr(self.partials), _lib.ptr(self.norm_scale), _lib.stream_of(self.partials)),
-            "sgd_clip")
+        _lib.check(_lib.lib().tlod_sgd_clip_pack_f32(
+            _lib.ptr(chunks), n, n_update, _lib.ptr(tiles), n_tiles, float(grad_scale),
+            self.momentum, self.clip_norm, _lib.ptr(self.partials), _lib.ptr(self.norm_scale),
+            _lib.stream_of(self.partials)), "sgd_clip")
         return self.norm_scale[0]
