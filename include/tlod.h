@@ -351,6 +351,16 @@ int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c
 int tlod_gemm_bs_ex_f32(const float* a, const float* b, const float* bias, const float* residual,
                         int relu, float* c, int M, int N, int K, int a_kcontig, int b_kcontig,
                         int nprod, void* ws, size_t ws_bytes, tlod_stream_t stream);
+/* The input gradient of a GEMM whose input is a ReLU output (the ResNet RoI head's bottleneck
+ * convs as GEMMs, lib/DAF/resnet.py Bottleneck.backward through relu(bn1(conv1(x))) ...):
+ * c = (a.b + residual) * (mask > 0) — residual (M x N, may be NULL): the identity shortcut's
+ * gradient added first; mask (M x N): the ReLU output the GEMM's input is.  One GEMM instead
+ * of the GEMM, autograd's sum of the two gradients and a ReLU-backward pass.  Same
+ * workspace as tlod_gemm_bs_f32; residual and mask must not alias c. */
+int tlod_gemm_bs_mask_f32(const float* a, const float* b, const float* residual,
+                          const float* mask, float* c, int M, int N, int K, int a_kcontig,
+                          int b_kcontig, int nprod, void* ws, size_t ws_bytes,
+                          tlod_stream_t stream);
 
 /* Split-bf16 3x3 convolution as an implicit GEMM over (c, tap) x flattened pixels, for
  * wide outputs (Cout >= 256): the forward of tlod_conv_fwd_ex_f32 (w_layout = 0: w is the
@@ -432,6 +442,10 @@ int tlod_im2col3x3_nhwc_f32(const float* x, int R, int H, int W, int C, float* c
                             tlod_stream_t stream);
 int tlod_col2im3x3_nhwc_f32(const float* col, int R, int H, int W, int C, float* dx,
                             tlod_stream_t stream);
+/* col2im with the previous layer's ReLU backward: dx = col2im(col) * (mask > 0), mask the
+ * (R, H, W, C) ReLU output that was im2col's input (may be NULL). */
+int tlod_col2im3x3_nhwc_mask_f32(const float* col, int R, int H, int W, int C, const float* mask,
+                                 float* dx, tlod_stream_t stream);
 
 
 /* ------------------------------------------------------------------ Optimiser step

@@ -141,13 +141,56 @@ def test_bottleneck_head_nhwc(inplanes, planes, stride, R):
     x = torch.randn(R, inplanes, H, H, generator=g)
     xd = x.to(dev).requires_grad_(True)
     xr = x.clone().requires_grad_(True)
-    y = db.forward_nhwc(xd.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+    y2, shp = db.forward_nhwc(xd.permute(0, 2, 3, 1))
+    y = y2.view(*shp, -1).permute(0, 3, 1, 2)
     yr = ob(xr)
     _close(y, yr, 1e-5)
     gy = torch.randn(y.shape, generator=g)
     y.backward(gy.to(dev))
     yr.backward(gy)
     _close(xd.grad, xr.grad, 1e-4)
+
+
+@pytest.mark.parametrize("R,entry", [(37, True), (5, False)])
+def test_head_fused_backward_bit_identical(R, entry, monkeypatch):
+    """The RoI head's fused backward (TLOD_HEAD_FUSE=1: each ReLU mask in the consumer's
+    input-gradient epilogue — tlod_gemm_bs_mask_f32, tlod_col2im3x3_nhwc_mask_f32 — and the
+    identity shortcut's gradient added in conv1's input-gradient GEMM) against the unfused
+    chain (torch.where masks, autograd's sum), over layer4's three bottlenecks: output, input
+    gradient and every weight / bias gradient bit for bit.  entry: the head-entry input
+    (already subsampled, 4x4) or the 7x7 map."""
+    from tlod import linear
+    from tlod.detector.resnet import ResNetTop, HeadEntry, _make_layer
+    g = torch.Generator().manual_seed(R)
+    layer = _make_layer(1024, 512, 3, stride=2)
+    for m in layer.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            _rand_bn(m, g)
+            for p in m.parameters():
+                p.requires_grad = False
+        elif isinstance(m, torch.nn.Conv2d):
+            with torch.no_grad():
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * (2.0 / m.weight[0].numel()) ** 0.5)
+    top = ResNetTop(layer).to(dev)
+    H = 4 if entry else 7
+    x = torch.randn(R, H, H, 1024, generator=g).to(dev)
+    gy = torch.randn(R, 2048, generator=g).to(dev)
+
+    def run(fuse):
+        monkeypatch.setenv("TLOD_HEAD_FUSE", fuse)
+        for p in top.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        y = top(HeadEntry(xi) if entry else xi.permute(0, 3, 1, 2))
+        (y.mean(2).mean(1) * gy).sum().backward()
+        return [y.detach(), xi.grad] + [p.grad for p in top.parameters() if p.requires_grad]
+    before = dict(linear.STATS)
+    fused = run("1")
+    assert linear.STATS["masked_dgrad"] - before["masked_dgrad"] == 5  # 3 x conv3 + 2 x conv1
+    assert linear.STATS["relu_bwd_skipped"] - before["relu_bwd_skipped"] == 8  # + 3 x conv1 (col2im)
+    plain = run("0")
+    for i, (a, b) in enumerate(zip(fused, plain)):
+        assert torch.equal(a, b), i
 
 
 LOSSES = ["rpn_loss_cls", "rpn_loss_box", "RCNN_loss_cls", "RCNN_loss_bbox", "DA_img_loss_cls",

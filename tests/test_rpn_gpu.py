@@ -108,6 +108,57 @@ def test_anchor_target_device_rng_distribution():
     del full
 
 
+def _rng_key(seed, stream, idx):
+    """(rng_u64(seed, stream, idx) >> 32) of csrc/common.h (splitmix64 twice), in numpy."""
+    def mix(z):
+        z = z + np.uint64(0x9e3779b97f4a7c15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
+    with np.errstate(over="ignore"):
+        base = mix(np.array([seed], np.uint64) ^ (np.array([stream], np.uint64) *
+                                                  np.uint64(0xd1b54a32d192ed03)))
+        return (mix(base + idx.astype(np.uint64)) >> np.uint64(32)).astype(np.uint32)
+
+
+@pytest.mark.parametrize("H,W,seed", [(37, 75, 5), (38, 75, 77), (20, 30, 3), (50, 100, 9)])
+def test_anchor_target_device_rng_exact_subset(H, W, seed):
+    """Production mode pinned exactly: the kept fg / bg anchors are the candidates whose
+    (key, anchor index) pairs are NOT among the m smallest, key = rng_u64(seed, 2b (fg) /
+    2b + 1 (bg), anchor) >> 32 — restated here in numpy.  (37, 75), (38, 75): the
+    LDS-key kernel (N = 33300 / 34200 anchors); (50, 100): N = 60000, the list kernel."""
+    from tlod.rpn.anchor_target import anchor_target, rpn_cfg_struct
+    from tlod.config import setup_training_cfg
+    setup_training_cfg("vgg16")
+    rng = np.random.default_rng(seed)
+    gts = gt_set(rng, G=50, W=W * 16, H=H * 16)[None]
+    gts[0, :, 2:4] = np.maximum(gts[0, :, 2:4], gts[0, :, 0:2] + 200)  # big boxes: many fg
+    gts[0, :, 2] = np.minimum(gts[0, :, 2], W * 16 - 1)
+    gts[0, :, 3] = np.minimum(gts[0, :, 3], H * 16 - 1)
+    im_info = np.array([[H * 16, W * 16, 1.0]], np.float32)
+    ident = type("N", (), {"permutation": lambda self, n: np.arange(n)})()
+    cfg = dict(orpn.DEFAULT_RPN)
+    cfg["batch"] = 10 ** 9  # no subsampling: the candidates
+    cand = orpn.anchor_target(H, W, gts, im_info, BASE, 16, ident, cfg)[0].ravel()
+    t = lambda x: torch.from_numpy(x).to(dev)
+    lab = anchor_target(t(BASE), H, W, 16, t(gts), t(im_info), rpn_cfg_struct(),
+                        seed=seed)[0].reshape(-1).cpu().numpy()
+    A, HW = BASE.shape[0], H * W
+    p = np.arange(A * HW)
+    idx = (p % HW) * A + p // HW  # output (a, h, w) -> the kernels' anchor index (h, w, a)
+    exp = cand.copy()
+    fg = np.nonzero(cand == 1)[0]
+    m_fg = max(0, len(fg) - 128)
+    k = _rng_key(seed, 0, idx[fg])
+    exp[fg[np.lexsort((idx[fg], k))[:m_fg]]] = -1
+    bg = np.nonzero(cand == 0)[0]
+    m_bg = len(bg) - (256 - min(len(fg), 128))
+    assert m_bg > 0
+    k = _rng_key(seed, 1, idx[bg])
+    exp[bg[np.lexsort((idx[bg], k))[:m_bg]]] = -1
+    np.testing.assert_array_equal(lab, exp)
+
+
 @pytest.mark.parametrize("seed,G,R", [(0, 8, 2000), (1, 30, 2000), (2, 2, 300), (3, 8, 128)])
 def test_proposal_target_replay_bit_exact(seed, G, R):
     from tlod.rpn.proposal_target import proposal_target, rcnn_cfg_struct

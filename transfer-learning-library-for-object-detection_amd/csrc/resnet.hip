@@ -139,7 +139,8 @@ __global__ void im2col3x3_nhwc_kernel(const float4* __restrict__ x, int H, int W
 }
 
 __global__ void col2im3x3_nhwc_kernel(const float4* __restrict__ col, int H, int W, int C4,
-                                      size_t total, float4* __restrict__ dx) {
+                                      size_t total, const float4* __restrict__ mask,
+                                      float4* __restrict__ dx) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4);
@@ -154,6 +155,13 @@ __global__ void col2im3x3_nhwc_kernel(const float4* __restrict__ col, int H, int
         const float4 v = col[(((r * H + oh) * W + ow) * 9 + t) * C4 + c];
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
+    }
+    if (mask != nullptr) {  // the previous layer's ReLU backward (its output is x)
+      const float4 m = mask[i];
+      a.x = m.x > 0.f ? a.x : 0.f;
+      a.y = m.y > 0.f ? a.y : 0.f;
+      a.z = m.z > 0.f ? a.z : 0.f;
+      a.w = m.w > 0.f ? a.w : 0.f;
     }
     dx[i] = a;
   }
@@ -198,17 +206,23 @@ extern "C" int tlod_im2col3x3_nhwc_f32(const float* x, int R, int H, int W, int 
   return kOk;
 }
 
-extern "C" int tlod_col2im3x3_nhwc_f32(const float* col, int R, int H, int W, int C, float* dx,
-                                      tlod_stream_t stream) {
+extern "C" int tlod_col2im3x3_nhwc_mask_f32(const float* col, int R, int H, int W, int C,
+                                           const float* mask, float* dx, tlod_stream_t stream) {
   TLOD_CHECK_ARG(R > 0 && H > 0 && W > 0 && C > 0 && (C & 3) == 0 && col && dx, "bad arguments");
-  TLOD_CHECK_ARG(((reinterpret_cast<uintptr_t>(col) | reinterpret_cast<uintptr_t>(dx)) & 15) == 0,
+  TLOD_CHECK_ARG(((reinterpret_cast<uintptr_t>(col) | reinterpret_cast<uintptr_t>(dx) |
+                   reinterpret_cast<uintptr_t>(mask)) & 15) == 0,
                  "16-B aligned tensors");
   const size_t total = (size_t)R * H * W * (C / 4);
   hipLaunchKernelGGL(col2im3x3_nhwc_kernel, dim3(grid_for(total)), dim3(256), 0,
                      (hipStream_t)stream, reinterpret_cast<const float4*>(col), H, W, C / 4, total,
-                     reinterpret_cast<float4*>(dx));
+                     reinterpret_cast<const float4*>(mask), reinterpret_cast<float4*>(dx));
   TLOD_LAUNCH_CHECK();
   return kOk;
+}
+
+extern "C" int tlod_col2im3x3_nhwc_f32(const float* col, int R, int H, int W, int C, float* dx,
+                                      tlod_stream_t stream) {
+  return tlod_col2im3x3_nhwc_mask_f32(col, R, H, W, C, nullptr, dx, stream);
 }
 
 extern "C" int tlod_stem_conv7x7s2_f32(const float* x, const float* weight, const float* scale,

@@ -359,6 +359,141 @@ __global__ void __launch_bounds__(kBlk) at_sample_kernel(int N, tlod_rpn_cfg cfg
   if (threadIdx.x == 0) nex[b] = c;
 }
 
+// The same subsampling with the labels held as per-thread bitmasks and the candidates' keys
+// in LDS (N <= kAtMax anchors, device RNG): thread t owns anchors t + kBlk j, so every label
+// is read and written once, coalesced, and every key is hashed once — the list-based kernel
+// above re-reads the list from memory and re-hashes every candidate in each of its six
+// passes, a chain of dependent loads that made it ~85 us of the step's critical path.  Same
+// result: the m picked candidates are the m smallest (key, anchor index) pairs — keys below
+// the radix-selected threshold T, then the need_eq smallest anchor indices among keys == T
+// (block_random_subset takes ties in list order, which is anchor order).
+constexpr int kAtSlots = 38;                  // anchors per thread (keys: 152 KB of LDS)
+constexpr int kAtMax = kBlk * kAtSlots;       // 38912 (12 x 38 x 75 = 34200 at 600 x 1200)
+
+template <class Act>
+__device__ void lds_random_subset(const uint32_t* __restrict__ skey, uint64_t cand, int n, int m,
+                                  Act act) {
+  if (m <= 0) return;
+  const int t = threadIdx.x;
+  if (m >= n) {
+#pragma unroll
+    for (int j = 0; j < kAtSlots; ++j)
+      if ((cand >> j) & 1ull) act(j);
+    return;
+  }
+  __shared__ int hist[256];
+  __shared__ uint32_t s_prefix;
+  __shared__ int s_need, s_min;
+  if (t == 0) { s_prefix = 0; s_need = m; }
+  __syncthreads();
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_prefix;
+    const uint32_t pmask = pass == 0 ? 0u : (0xffffffffu << (32 - 8 * pass));
+#pragma unroll 8
+    for (int j = 0; j < kAtSlots; ++j) {
+      const uint32_t k = skey[j * kBlk + t];
+      if (((cand >> j) & 1ull) && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (t < 64) {  // the digit whose cumulative count reaches `need` (as block_random_subset)
+      const int need = s_need;
+      const int h0 = hist[4 * t], h1 = hist[4 * t + 1], h2 = hist[4 * t + 2], h3 = hist[4 * t + 3];
+      const int sl = h0 + h1 + h2 + h3;
+      int incl = sl;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (t >= o) incl += y;
+      }
+      int acc = incl - sl;
+      if (acc < need && need <= incl) {
+        int d = 4 * t;
+        if (acc + h0 < need) { acc += h0; ++d;
+          if (acc + h1 < need) { acc += h1; ++d;
+            if (acc + h2 < need) { acc += h2; ++d; } } }
+        s_need = need - acc;
+        s_prefix = prefix | ((uint32_t)d << shift);
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t T = s_prefix;
+  int need_eq = s_need;
+  uint64_t tie = 0;
+#pragma unroll
+  for (int j = 0; j < kAtSlots; ++j) {
+    if (!((cand >> j) & 1ull)) continue;
+    const uint32_t k = skey[j * kBlk + t];
+    if (k < T) act(j);
+    else if (k == T) tie |= 1ull << j;
+  }
+  if (block_sum(__popcll(tie)) <= need_eq) {  // (the common case: every tie is picked)
+#pragma unroll
+    for (int j = 0; j < kAtSlots; ++j)
+      if ((tie >> j) & 1ull) act(j);
+    return;
+  }
+  for (; need_eq > 0; --need_eq) {  // the smallest anchor indices among the ties, one by one
+    if (t == 0) s_min = 0x7fffffff;
+    __syncthreads();
+    if (tie) atomicMin(&s_min, t + kBlk * (__ffsll((unsigned long long)tie) - 1));
+    __syncthreads();
+    const int w = s_min;
+    if (w % kBlk == t) {
+#pragma unroll
+      for (int j = 0; j < kAtSlots; ++j)  // (static slot indices: the caller's masks stay in registers)
+        if (j == w / kBlk) act(j);
+      tie &= ~(1ull << (w / kBlk));
+    }
+    __syncthreads();
+  }
+}
+
+// dynamic LDS: kBlk * kAtSlots keys
+__global__ void __launch_bounds__(kBlk) at_sample_lds_kernel(int N, tlod_rpn_cfg cfg, uint64_t seed,
+                                                             int8_t* __restrict__ label_all,
+                                                             int32_t* __restrict__ nex) {
+  extern __shared__ uint32_t skey[];
+  const int b = blockIdx.x, t = threadIdx.x;
+  int8_t* label = label_all + (size_t)b * N;
+  uint64_t fgm = 0, bgm = 0;  // slot j: label 1 / label 0 (else -1)
+#pragma unroll
+  for (int j = 0; j < kAtSlots; ++j) {
+    const int i = t + kBlk * j;
+    const int l = i < N ? label[i] : -1;
+    fgm |= (uint64_t)(l == 1) << j;
+    bgm |= (uint64_t)(l == 0) << j;
+  }
+  const int num_fg = (int)(cfg.fg_fraction * (float)cfg.batch_size);
+  const int nfg = block_sum(__popcll(fgm));
+  if (nfg > num_fg) {
+#pragma unroll 4
+    for (int j = 0; j < kAtSlots; ++j)
+      if ((fgm >> j) & 1ull)
+        skey[j * kBlk + t] = (uint32_t)(rng_u64(seed, 2ull * b, (uint64_t)(t + kBlk * j)) >> 32);
+    lds_random_subset(skey, fgm, nfg, nfg - num_fg, [&](int j) { fgm &= ~(1ull << j); });
+    __syncthreads();
+  }
+  const int num_bg = cfg.batch_size - (nfg > num_fg ? num_fg : nfg);
+  const int nbg = block_sum(__popcll(bgm));
+  if (nbg > num_bg) {
+#pragma unroll 4
+    for (int j = 0; j < kAtSlots; ++j)
+      if ((bgm >> j) & 1ull)
+        skey[j * kBlk + t] = (uint32_t)(rng_u64(seed, 2ull * b + 1, (uint64_t)(t + kBlk * j)) >> 32);
+    lds_random_subset(skey, bgm, nbg, nbg - num_bg, [&](int j) { bgm &= ~(1ull << j); });
+  }
+#pragma unroll
+  for (int j = 0; j < kAtSlots; ++j) {
+    const int i = t + kBlk * j;
+    if (i < N) label[i] = (int8_t)(((fgm >> j) & 1ull) ? 1 : (((bgm >> j) & 1ull) ? 0 : -1));
+  }
+  const int c = block_sum(__popcll(fgm) + __popcll(bgm));
+  if (t == 0) nex[b] = c;
+}
+
 // grid (ceil(N/256), B): targets, weights, unmap, output layouts (:147-191).
 __global__ void __launch_bounds__(256) at_output_kernel(
     AnchorGeo geo, const float* __restrict__ gt, int G, int B, float inside_weight,
@@ -627,8 +762,15 @@ extern "C" int tlod_anchor_target_sample_f32(const float* base_anchors, int A, i
   carve_at(c, w, B, N, G);
   if (!c.ok()) { set_error("tlod_anchor_target: workspace too small"); return kWorkspace; }
   AnchorGeo geo{base_anchors, A, H, W, feat_stride};
-  hipLaunchKernelGGL(at_sample_kernel, dim3(B), dim3(kBlk), 0, s, N, *cfg, perm, perm_off, seed,
-                     w.label, w.list, w.nex);
+  if (perm == nullptr && N <= kAtMax) {
+    const int lds = kAtMax * (int)sizeof(uint32_t);
+    TLOD_HIP(lds_attr((const void*)at_sample_lds_kernel, lds));
+    hipLaunchKernelGGL(at_sample_lds_kernel, dim3(B), dim3(kBlk), lds, s, N, *cfg, seed, w.label,
+                       w.nex);
+  } else {
+    hipLaunchKernelGGL(at_sample_kernel, dim3(B), dim3(kBlk), 0, s, N, *cfg, perm, perm_off, seed,
+                       w.label, w.list, w.nex);
+  }
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(at_output_kernel, dim3(div_up(N, 256), B), dim3(256), 0, s, geo, gt_boxes, G,
                      B, cfg->inside_weight, w.label, w.argmax, w.nex, labels, bbox_targets,

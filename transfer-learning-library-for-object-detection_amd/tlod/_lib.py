@@ -119,6 +119,8 @@ SIGNATURES = {
                                  c_size_t, P]),
     "tlod_gemm_bs_ex_f32": (c_int, [P, P, P, P, c_int, P, c_int, c_int, c_int, c_int, c_int,
                                     c_int, P, c_size_t, P]),
+    "tlod_gemm_bs_mask_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      P, c_size_t, P]),
     "tlod_conv3x3_gemm_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
                                                         c_int]),
     "tlod_conv3x3_gemm_bs_f32": (c_int, [P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int,
@@ -138,6 +140,7 @@ SIGNATURES = {
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_im2col3x3_nhwc_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_col2im3x3_nhwc_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_col2im3x3_nhwc_mask_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "tlod_image_blob_u8": (c_int, [P, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_int, P, P]),
     "tlod_detect_f32": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_float, c_float, c_float,

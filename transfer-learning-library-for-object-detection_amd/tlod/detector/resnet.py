@@ -81,32 +81,44 @@ class Subsample2Function(torch.autograd.Function):
 
 class Im2col3x3Function(torch.autograd.Function):
     """x (R,H,W,C) channels-last -> (R*H*W, 9*C) taps in (kh, kw, c) order, zero padding 1
-    (tlod_im2col3x3_nhwc_f32; backward tlod_col2im3x3_nhwc_f32)."""
+    (tlod_im2col3x3_nhwc_f32; backward tlod_col2im3x3_nhwc_f32).  shape (R, H, W): x is the
+    same map as (R*H*W, C) rows (the head's GEMM outputs, no autograd view in between);
+    relu_in: x is a ReLU output, so the backward applies its mask in the col2im pass
+    (tlod_col2im3x3_nhwc_mask_f32) and tags the gradient for LinearActFunction."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, shape=None, relu_in=False):
         _lib.require_cuda(x)
         x = x.contiguous()
-        R, H, W, C = x.shape
+        R, H, W = shape if shape is not None else x.shape[:3]
+        C = x.shape[-1]
         col = torch.empty((R * H * W, 9 * C), dtype=x.dtype, device=x.device)
         _lib.check(_lib.lib().tlod_im2col3x3_nhwc_f32(_lib.ptr(x), R, H, W, C, _lib.ptr(col),
                                                       _lib.stream_of(x)), "im2col3x3_nhwc")
-        ctx.shape = (R, H, W, C)
+        ctx.shape, ctx.in_shape = (R, H, W, C), x.shape
+        ctx.save_for_backward(x if relu_in else None)
         return col
 
     @staticmethod
     def backward(ctx, g):
         R, H, W, C = ctx.shape
+        (x,) = ctx.saved_tensors
         g = g.contiguous()
-        dx = torch.empty((R, H, W, C), dtype=g.dtype, device=g.device)
-        _lib.check(_lib.lib().tlod_col2im3x3_nhwc_f32(_lib.ptr(g), R, H, W, C, _lib.ptr(dx),
-                                                      _lib.stream_of(g)), "col2im3x3_nhwc")
-        return dx
+        dx = torch.empty(ctx.in_shape, dtype=g.dtype, device=g.device)
+        _lib.check(_lib.lib().tlod_col2im3x3_nhwc_mask_f32(
+            _lib.ptr(g), R, H, W, C, _lib.ptr(x), _lib.ptr(dx), _lib.stream_of(g)),
+            "col2im3x3_nhwc")
+        if x is not None:
+            dx._tlod_relu_masked = (x.data_ptr(), dx.data_ptr(), dx._version)
+        return dx, None, None
 
 
-def im2col3x3_nhwc(x):
-    if x.shape[3] % 4 == 0:
-        return Im2col3x3Function.apply(x)
+def im2col3x3_nhwc(x, shape=None, relu_in=False):
+    """x: (R, H, W, C), or (R*H*W, C) rows with shape = (R, H, W)."""
+    if x.shape[-1] % 4 == 0:
+        return Im2col3x3Function.apply(x, shape, relu_in)
+    if shape is not None:
+        x = x.view(*shape, x.shape[-1])
     R, H, W, P = x.shape  # (unaligned channel counts: the torch composition)
     pad = F.pad(x, (0, 0, 1, 1, 1, 1))
     return torch.cat([pad[:, kh:kh + H, kw:kw + W, :] for kh in range(3) for kw in range(3)],
@@ -168,8 +180,11 @@ class Bottleneck(nn.Module):
 
     # ---------------------------------------------------------------- RoI head path
     @staticmethod
-    def _gemm_bn(xm, conv, bn, relu, residual=None):
-        """xm: (P, Cin) channels-last rows; conv as a GEMM + folded BN (+res) (+ReLU)."""
+    def _gemm_bn(xm, conv, bn, relu, residual=None, relu_in=False, link=None, role=0):
+        """xm: (P, Cin) channels-last rows; conv as a GEMM + folded BN (+res) (+ReLU).
+        relu_in: xm is a ReLU output (its input gradient is masked in the GEMM epilogue);
+        link / role: the identity shortcut's gradient handed from conv3 (role 3) to conv1
+        (role 1) — see LinearActFunction."""
         scale, shift = fold_bn(bn)
         w = conv.weight
         wm = w.view(w.shape[0], -1) if w.shape[2] == 1 else w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
@@ -186,25 +201,37 @@ class Bottleneck(nn.Module):
             return LinearFunction.apply(xm.contiguous(), wm * scale[:, None], shift, m)
         # residual add and ReLU in the GEMM epilogue (tlod_gemm_bs_ex_f32)
         return LinearActFunction.apply(xm.contiguous(), wm * scale[:, None], shift, residual,
-                                       relu, m)
+                                       relu, m, relu_in, link, role)
 
-    def forward_nhwc(self, x, subsampled=False):
-        """x: (R, H, W, C) channels-last (the layer4 RoI head); subsampled: x is already the
-        stride-2 subsample (the head entry, HeadEntry)."""
-        if self.stride == 2 and not subsampled:
-            x = x[:, ::2, ::2, :]
-        R, H, W, C = x.shape
-        xm = x.reshape(R * H * W, C)
-        out = self._gemm_bn(xm, self.conv1, self.bn1, relu=True)
+    def forward_nhwc(self, x, subsampled=False, shape=None, relu_in=False):
+        """The layer4 RoI head, channels-last.  x: (R, H, W, C), or (R*H*W, C) rows with
+        shape = (R, H, W) (a previous block's output, relu_in = True); returns (rows, shape).
+        subsampled: x is already the stride-2 subsample (the head entry, HeadEntry)."""
+        if shape is None:
+            if self.stride == 2 and not subsampled:
+                x = x[:, ::2, ::2, :]
+            R, H, W, C = x.shape
+            xm = x.reshape(R * H * W, C)
+        else:
+            assert self.stride == 1 or subsampled
+            (R, H, W), xm = shape, x
+        fused = linear_math() != "f32" and os.environ.get("TLOD_HEAD_FUSE", "1") != "0"
+        # identity shortcut: conv1's input gradient takes the shortcut's gradient (HeadLink)
+        link = (ShortcutLink() if fused and self.downsample is None and self.stride == 1
+                else None)
+        out = self._gemm_bn(xm, self.conv1, self.bn1, relu=True, relu_in=fused and relu_in,
+                            link=link, role=1)
         P = out.shape[1]
         self._tap("r1", out.view(R, H, W, P), nhwc=True)
-        taps = im2col3x3_nhwc(out.view(R, H, W, P))
+        taps = im2col3x3_nhwc(out, (R, H, W), relu_in=fused)
         out = self._gemm_bn(taps, self.conv2, self.bn2, relu=True)
         self._tap("r2", out.view(R, H, W, P), nhwc=True)
         res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False)
                if self.downsample is not None else xm)
-        out = self._gemm_bn(out, self.conv3, self.bn3, relu=True, residual=res)
-        return self._tap("r3", out.view(R, H, W, -1), nhwc=True)
+        out = self._gemm_bn(out, self.conv3, self.bn3, relu=True, residual=res, relu_in=fused,
+                            link=link, role=3)
+        self._tap("r3", out.view(R, H, W, -1), nhwc=True)
+        return out, (R, H, W)
 
 
 class ResNetBase(nn.Sequential):
@@ -266,9 +293,11 @@ class ResNetTop(nn.Sequential):
             x, sub = pool5.x, True
         else:
             x, sub = pool5.permute(0, 2, 3, 1), False
+        shape = None
         for i, block in enumerate(self[0]):
-            x = block.forward_nhwc(x, subsampled=sub and i == 0)
-        return x
+            x, shape = block.forward_nhwc(x, subsampled=sub and i == 0,
+                                          shape=shape, relu_in=shape is not None)
+        return x.view(*shape, x.shape[-1])
 
 
 def _make_layer(inplanes, planes, blocks, stride=1):

@@ -93,20 +93,54 @@ class LinearFunction(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def gemm_mask(a, b, M, N, K, a_kcontig, b_kcontig, mask, residual=None, math="bf16x6"):
+    """c = (A.B (+ residual)) * (mask > 0): an input gradient through the ReLU whose output
+    (mask) the GEMM read, with an identity shortcut's gradient added first
+    (tlod_gemm_bs_mask_f32).  The result is tagged for LinearActFunction's backward."""
+    a, b = a.contiguous(), b.contiguous()
+    mask = mask.detach().contiguous()
+    nprod = 6 if math == "bf16x6" else 3
+    L = _lib.lib()
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    ws = _lib.workspace(L.tlod_gemm_bs_workspace_bytes(M, N, K, a_kcontig, b_kcontig, nprod),
+                        a.device, "gemm")
+    if residual is not None:
+        residual = residual.detach().contiguous()
+        assert residual.shape == (M, N)
+    from .conv import _timed
+    _timed("gemm", (M, N, K), lambda: _lib.check(
+        L.tlod_gemm_bs_mask_f32(_lib.ptr(a), _lib.ptr(b), _lib.ptr(residual), _lib.ptr(mask),
+                                _lib.ptr(c), M, N, K, int(a_kcontig), int(b_kcontig), nprod,
+                                _lib.ptr(ws), ws.numel(), _lib.stream_of(a)), "gemm_bs_mask"),
+        math)
+    c._tlod_relu_masked = (mask.data_ptr(), c.data_ptr(), c._version)
+    STATS["masked_dgrad"] += 1
+    return c
+
+
+STATS = {"masked_dgrad": 0, "relu_bwd_skipped": 0}  # fused ReLU-backward counters (tests)
+
+
 class LinearActFunction(torch.autograd.Function):
     """y = act(x W^T + bias + residual) in one GEMM launch (the ResNet RoI head's bottleneck
     convs as GEMMs with the folded BN shift as the bias, lib/DAF/resnet.py Bottleneck:
     out = relu(bn3(conv3(...)) + residual)).  Backward: g = dy * (y > 0), then the GEMMs of
-    LinearFunction; the residual's gradient is g."""
+    LinearFunction; the residual's gradient is g.
+    relu_in: x is a ReLU output — the input gradient is masked in the GEMM epilogue
+    (gemm_mask) and tagged, so that layer's backward skips its own mask pass (a gradient that
+    arrives tagged for this y is already g).  link (a tlod.conv.ShortcutLink) / role: an
+    identity bottleneck's conv3 (role 3) hands its residual gradient g to conv1 (role 1),
+    whose input gradient adds it in the same epilogue — no autograd sum of the two."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, relu, math):
+    def forward(ctx, x, weight, bias, residual, relu, math, relu_in=False, link=None, role=0):
         R, I = x.shape
         O = weight.shape[0]
         y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math, residual=residual, relu=relu)
         ctx.math, ctx.relu = math, relu
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
         ctx.params = (weight, bias)
+        ctx.relu_in, ctx.link, ctx.role = bool(relu_in), link, role
         ctx.save_for_backward(x, weight, y if relu else None)
         return y
 
@@ -115,19 +149,32 @@ class LinearActFunction(torch.autograd.Function):
         x, weight, y = ctx.saved_tensors
         R, I = x.shape
         O = weight.shape[0]
-        g = dy.contiguous()
-        if ctx.relu:
-            g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        if ctx.relu and getattr(dy, "_tlod_relu_masked", None) == (y.data_ptr(), dy.data_ptr(),
+                                                                   dy._version):
+            g = dy  # masked by the consumer's input-gradient epilogue
+            STATS["relu_bwd_skipped"] += 1
+        elif ctx.relu:  # (one pass: dy may be a broadcast view, e.g. the head's mean backward)
+            g = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+        else:
+            g = dy.contiguous()
+        res = None
+        if ctx.role == 1 and ctx.link is not None:
+            res, ctx.link.g = ctx.link.g, None
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math)
+            if ctx.relu_in:
+                dx = gemm_mask(g, weight.detach(), R, I, O, 1, 0, x, res, ctx.math)
+            else:
+                dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math, residual=res)
         if ctx.needs_input_grad[1]:
             dw = gemm(g, x, O, I, R, 0, 0, None, ctx.math, out=grad_out(ctx.params[0]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             slot = grad_out(ctx.params[1])
             db = g.sum(0) if slot is None else torch.sum(g, 0, out=slot)
         dres = g if ctx.has_res and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None, None
+        if dres is not None and ctx.role == 3 and ctx.link is not None:
+            ctx.link.g, dres = dres, None  # to conv1's backward
+        return dx, dw, db, dres, None, None, None, None, None
 
 
 class Linear(nn.Linear):
