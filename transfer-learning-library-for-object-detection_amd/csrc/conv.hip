@@ -40,12 +40,6 @@ namespace tlod {
 #ifndef TLOD_CONV_SGB_W
 #define TLOD_CONV_SGB_W 0
 #endif
-// Split-bf16 kernels: store the next chunk's staged operands to the other LDS buffer in
-// the middle of the MFMA phase (the other wave of the SIMD keeps the MFMA pipe busy while
-// this one splits and writes) instead of after it.  0 = after the MFMA phase.
-#ifndef TLOD_MID_STORE
-#define TLOD_MID_STORE 1
-#endif
 // Split-bf16 forward: pair the 9 taps across consecutive input-channel chunks instead of
 // padding each chunk to 10 tap slots (0 = pad, for A/B).
 #ifndef TLOD_WG_SWZ
@@ -612,14 +606,20 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_fwd_bs_kernel(
       const bool more2 = c + 2 < c_end;
 #pragma unroll
       for (int st = 0; st < 9; ++st) {
+        // (sched_barrier: the staging stays between the k-steps it was placed at — the
+        // compiler otherwise sinks it below the remaining MFMAs, as in gemm.hip's K loop)
         if (st == 2) {
+          __builtin_amdgcn_sched_barrier(0);
           store_chunk(smem + C::BUF);
           if (more2) load_chunk(c + 2);
+          __builtin_amdgcn_sched_barrier(0);
         }
         if (st == 4 || st == 5) __syncthreads();
         if (st == 6 && more2) {
+          __builtin_amdgcn_sched_barrier(0);
           store_chunk(smem);
           if (c + 3 < c_end) load_chunk(c + 3);
+          __builtin_amdgcn_sched_barrier(0);
         }
         step(smem, a_row + (khalf ? unit_a(2 * st + 1) : unit_a(2 * st)),
              b_lane + (khalf ? unit_b(2 * st + 1) : unit_b(2 * st)));
@@ -1647,16 +1647,21 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
 
   const int a_rd = (wm * MI * 32 + l32) * C::PITCH + wg_slot(l32, 8 * khalf);
   const int b_rd = C::NPL * C::A_PLANE + (wn * NJ * 32 + l32) * C::PITCH + wg_slot(l32, 8 * khalf);
+  // chunk c + 1 is split + stored half way through chunk c's MFMAs, and the registers are
+  // reloaded with chunk c + 2 right after: every chunk's loads have a whole chunk of MFMAs to
+  // land.  sched_barrier keeps the staging there — the compiler otherwise sinks it (and its
+  // vmcnt wait) below the MFMAs, where the SIMD's two waves split while the matrix pipe idles
+  // (the same fix as gemm.hip's K loop).
   if (c_begin < c_end) {
     load_chunk(c_begin);
     store_chunk(smem);
+    if (c_begin + 1 < c_end) load_chunk(c_begin + 1);
   }
   __syncthreads();
   for (int c = c_begin; c < c_end; ++c) {
     const int it = c - c_begin;
     const unsigned char* buf = smem + (it & 1) * C::BUF;
     const bool more = c + 1 < c_end;
-    if (more) load_chunk(c + 1);
     u32x4 b[NJ][3];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -1665,17 +1670,21 @@ __global__ void __launch_bounds__(WM* WN * 64) TLOD_CONV_OCC conv_wgrad_bs_kerne
         b[j][pl] = *reinterpret_cast<const u32x4*>(buf + b_rd + pl * C::B_PLANE + j * 32 * C::PITCH);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      if (TLOD_MID_STORE && more && i == MI / 2) store_chunk(smem + ((it + 1) & 1) * C::BUF);
       u32x4 a[3];
 #pragma unroll
       for (int pl = 0; pl < C::NPL; ++pl)
         a[pl] = *reinterpret_cast<const u32x4*>(buf + a_rd + pl * C::A_PLANE + i * 32 * C::PITCH);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
+        if (more && i * NJ + j == MI * NJ / 2) {
+          __builtin_amdgcn_sched_barrier(0);
+          store_chunk(smem + ((it + 1) & 1) * C::BUF);
+          if (c + 2 < c_end) load_chunk(c + 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         bs_mac<NP>(acc[i][j], a[0], a[1], a[2], b[j][0], b[j][1], b[j][2]);
       }
     }
-    if (!TLOD_MID_STORE && more) store_chunk(smem + ((it + 1) & 1) * C::BUF);
     __syncthreads();
   }
 
