@@ -139,7 +139,11 @@ struct Stager {
     const unsigned* mm = S ? mask2 : mask;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      if (lds[i] < 0) continue;
+      // (a slot check only where a lane can lack a slot: the store stays branch-free, so the
+      // staging can be interleaved with the MFMAs of its basic block)
+      if constexpr (VECS % kNT != 0) {
+        if (lds[i] < 0) continue;
+      }
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = ((mm[i] >> e) & 1) ? rr[i][e] : 0.f;
@@ -290,13 +294,12 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
   for (int c = c_begin; c < c_end; ++c) {
     const int it = c - c_begin;
     const unsigned char* buf = smem + (it & 1) * BUF;
-    const bool more = c + 1 < c_end, more2 = c + 2 < c_end;
+    // (unconditional: past the range the loads read zeros — raw buffer range checks and the
+    // K masks — into the buffer nobody reads next, and the loop body stays one basic block)
     auto mid = [&]() {
       store(smem + ((it + 1) & 1) * BUF);
-      if (more2) {
-        sa.load((c + 2) * kTK, Ra);
-        sb.load((c + 2) * kTK, Rb);
-      }
+      sa.load((c + 2) * kTK, Ra);
+      sb.load((c + 2) * kTK, Rb);
     };
     if (TLOD_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
     u32x4 b[kNJ][3];
@@ -313,7 +316,7 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
         a[pl] = read_operand<AK>(buf + pl * A_PL, wm * MI * 32 + i * 32, lane);
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
-        if (more && i * kNJ + j == MI * kNJ / 2) {
+        if (i * kNJ + j == MI * kNJ / 2) {
           // kept half way through the MFMAs: the compiler otherwise sinks the split + stores
           // (and their vmcnt wait) below every MFMA, where the two waves of a SIMD split
           // together while the matrix pipe idles
