@@ -263,7 +263,8 @@ __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__
                                                        unsigned ncell,
                                                        unsigned* __restrict__ keys,
                                                        unsigned* __restrict__ vals,
-                                                       float2* __restrict__ geo) {
+                                                       float2* __restrict__ geo,
+                                                       int* __restrict__ trow, int QH, int QW) {
   const int ah = ph + 1, aw = pw + 1, S = ah * aw;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R * S) return;
@@ -277,6 +278,10 @@ __global__ void __launch_bounds__(256) rbg_geom_kernel(const float* __restrict__
   const bool ok = vy && vx;
   const unsigned c00 = (unsigned)(((int)ro[0] * H + y) * W + x);
   geo[i] = make_float2(hr, wr);
+  if (trow != nullptr) {  // S2: the output bin (2 hy, 2 hx) this sample feeds, or -1
+    const int hy = sy >> 1, hx = sx >> 1;
+    trow[i] = hy < QH && hx < QW ? (r * QH + hy) * QW + hx : -1;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     keys[4 * i + k] = ok ? c00 + (k >> 1) * W + (k & 1) : ncell;
@@ -345,7 +350,7 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
     const unsigned* __restrict__ vals, const float2* __restrict__ geo,
     const float* __restrict__ sg, int C, int ncell, float* __restrict__ acc,
     float* __restrict__ carry_head, float* __restrict__ carry_tail, int* __restrict__ flags,
-    int S, int aw, int QH, int QW) {
+    const int* __restrict__ trow) {
   const int lane = threadIdx.x & 63;
   const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = start[ncell];  // valid taps (sorted to the front)
@@ -356,10 +361,12 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
   const bool cok = c < C;
   unsigned kl = 0xffffffffu, vl = 0;
   float2 gl = make_float2(0.f, 0.f);
+  int tl = -1;
   if (lane < jn) {
     kl = keys[j0 + lane];
     vl = vals[j0 + lane];
     gl = geo[vl >> 2];
+    if constexpr (S2) tl = trow[vl >> 2];
   }
   const unsigned kprev = j0 > 0 ? keys[j0 - 1] : 0xffffffffu;
   const unsigned knext = j0 + jn < n ? keys[j0 + jn] : 0xffffffffu;
@@ -382,16 +389,15 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
     float sv[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
-      const unsigned vu = __builtin_amdgcn_readlane(vl, min(j + u, jn - 1));
       if constexpr (S2) {
         // (a sample past the last selected bin — the last row / column of an even bin count —
         // keeps its taps with value 0, so the taps and their segments are those of the
-        // zero-padded 7 x 7 backward: the same sums in the same association)
-        const int row = (int)(vu >> 2), r = row / S, smp = row - r * S;
-        const int hy = smp / aw >> 1, hx = (smp % aw) >> 1;
-        const bool cov = hy < QH && hx < QW;
-        sv[u] = cok && cov ? sg[((size_t)(r * QH + hy) * QW + hx) * C + c] * 0.25f : 0.f;  // = top / 4.f
+        // zero-padded 7 x 7 backward: the same sums in the same association; the bin row of
+        // each sample comes from rbg_geom_kernel, so no per-tap index arithmetic here)
+        const int tr = __builtin_amdgcn_readlane(tl, min(j + u, jn - 1));
+        sv[u] = cok && tr >= 0 ? sg[(size_t)tr * C + c] * 0.25f : 0.f;  // = top / 4.f
       } else {
+        const unsigned vu = __builtin_amdgcn_readlane(vl, min(j + u, jn - 1));
         sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
       }
     }
@@ -456,7 +462,7 @@ __global__ void __launch_bounds__(256) rbg_seg_fixup_kernel(
 struct RbgWs {
   unsigned *keys, *vals, *keys_s, *vals_s;
   float2* geo;
-  int *start, *flags;
+  int *start, *flags, *trow;
   float *sg, *acc, *carry_head, *carry_tail;
   void* cub_tmp;
   size_t cub_bytes;
@@ -470,6 +476,7 @@ static size_t carve_rbg(Carve& cv, RbgWs& w, int B, int C, int H, int W, int R, 
   w.keys_s = cv.take<unsigned>(n);
   w.vals_s = cv.take<unsigned>(n);
   w.geo = cv.take<float2>((size_t)R * S);
+  w.trow = s2 ? cv.take<int>((size_t)R * S) : nullptr;
   w.start = cv.take<int>((size_t)B * H * W + 1);
   w.sg = s2 ? nullptr : cv.take<float>((size_t)R * S * C);
   const size_t nseg = (n + 63) / 64;
@@ -725,7 +732,7 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     const int S = (ph + 1) * (pw + 1), n = R * S * 4;
     const unsigned ncell = (unsigned)ncell_sz;
     hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale,
-                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo);
+                       H, W, ph, pw, ncell, w.keys, w.vals, w.geo, (int*)nullptr, 0, 0);
     TLOD_LAUNCH_CHECK();
     size_t cb = w.cub_bytes;
     TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s,
@@ -740,7 +747,7 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     const int nseg = div_up(n, 64);
     hipLaunchKernelGGL(rbg_seg_gather_kernel<false>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256),
                        0, s, w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell, w.acc,
-                       w.carry_head, w.carry_tail, w.flags, S, pw + 1, 0, 0);
+                       w.carry_head, w.carry_tail, w.flags, (const int*)nullptr);
     TLOD_LAUNCH_CHECK();
     hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
                        w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
@@ -825,7 +832,7 @@ extern "C" int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, 
   const int QH = (ph + 1) / 2, QW = (pw + 1) / 2;
   const unsigned ncell = (unsigned)((size_t)B * H * W);
   hipLaunchKernelGGL(rbg_geom_kernel, dim3(div_up(R * S, 256)), dim3(256), 0, s, rois, R, scale, H,
-                     W, ph, pw, ncell, w.keys, w.vals, w.geo);
+                     W, ph, pw, ncell, w.keys, w.vals, w.geo, w.trow, QH, QW);
   TLOD_LAUNCH_CHECK();
   size_t cb = w.cub_bytes;
   TLOD_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, cb, w.keys, w.keys_s, w.vals, w.vals_s, n,
@@ -837,7 +844,7 @@ extern "C" int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, 
   const int nseg = div_up(n, 64);
   hipLaunchKernelGGL(rbg_seg_gather_kernel<true>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0,
                      s, w.start, w.keys_s, w.vals_s, w.geo, top_grad, C, (int)ncell, w.acc,
-                     w.carry_head, w.carry_tail, w.flags, S, pw + 1, QH, QW);
+                     w.carry_head, w.carry_tail, w.flags, w.trow);
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
                      w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
