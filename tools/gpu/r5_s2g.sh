@@ -9,8 +9,8 @@ for r in 1 2; do
   for v in new rhead; do
     L=""; [ $v != new ] && L=build_variants/$v/libtlod.so
     TLOD_LIB=$L timeout -k 10 400 python3 bench.py --method atf --net res101 --steps 8 --warmup 3 --cpu-baseline-steps 0 > $O/atf.$v.$r.json 2>/dev/null
-    TLOD_LIB=$L timeout -k 10 300 python3 bench.py --method daf --net res101 --cpu-baseline-steps 0 > $O/r101.$v.$r.json 2>/dev/null
-    echo "$v r$r atf $(python3 -c "import json;print(json.load(open('$O/atf.$v.$r.json'))['value'])") r101 $(python3 -c "import json;print(json.load(open('$O/r101.$v.$r.json'))['value'])")"
+    TLOD_LIB=$L timeout -k 10 300 python3 bench.py --cpu-baseline-steps 0 > $O/r101.$v.$r.json 2>/dev/null
+    echo "$v r$r atf $(python3 -c "import json;print(json.load(open('$O/atf.$v.$r.json'))['value'])") vgg $(python3 -c "import json;print(json.load(open('$O/r101.$v.$r.json'))['value'])")"
   done
 done
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

@@ -338,27 +338,62 @@ __device__ __forceinline__ float tap_value(float g, float hr, float wr, int k) {
   }
 }
 
-// grid (ceil(nseg / 4), ceil(C / 64)), 4 waves: wave = segment of 64 sorted taps, lane =
-// channel.  flags[seg]: 1 = owns a run continuing into the next segments (its tail piece in
-// carry_tail), 2 = one run covering the whole segment and continuing on both sides.
+// grid (ceil(nseg / 4), ceil(C / (64 V))), 4 waves: wave = segment of 64 sorted taps, lane =
+// V consecutive channels (V = 4: one 16-B load per tap and lane, so a wave keeps 16 rows x
+// 1 KB in flight instead of 16 x 256 B — the gather is bound by those dependent row loads;
+// every channel's arithmetic and order unchanged).  flags[seg]: 1 = owns a run continuing into
+// the next segments (its tail piece in carry_tail), 2 = one run covering the whole segment
+// and continuing on both sides.
 // S2 (the stride-2 head entry): no sample-gradient rows — sample (r, sy, sx) feeds exactly
 // one output bin, so its gradient is that bin's top row / 4, read straight from the
-// channels-last top gradient (R, QH, QW, C) (S = samples per RoI, aw = samples per row).
-template <bool S2>
+// channels-last top gradient (R, QH, QW, C); trow (from rbg_geom_kernel) names the row.
+template <int V>
+struct VecF;
+template <>
+struct VecF<1> {
+  typedef float T;
+  static __device__ __forceinline__ T zero() { return 0.f; }
+  static __device__ __forceinline__ T load(const float* p) { return *p; }
+  static __device__ __forceinline__ void store(float* p, T v) { *p = v; }
+};
+template <>
+struct VecF<4> {
+  typedef float4 T;
+  static __device__ __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ T load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static __device__ __forceinline__ void store(float* p, T v) { *reinterpret_cast<float4*>(p) = v; }
+};
+__device__ __forceinline__ float vscale(float v, float s) { return v * s; }
+__device__ __forceinline__ float4 vscale(float4 v, float s) {
+  return make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
+}
+__device__ __forceinline__ void vtap(float& a, float g, float hr, float wr, int k) {
+  a += tap_value(g, hr, wr, k);
+}
+__device__ __forceinline__ void vtap(float4& a, float4 g, float hr, float wr, int k) {
+  a.x += tap_value(g.x, hr, wr, k);
+  a.y += tap_value(g.y, hr, wr, k);
+  a.z += tap_value(g.z, hr, wr, k);
+  a.w += tap_value(g.w, hr, wr, k);
+}
+
+template <bool S2, int V>
 __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
     const int* __restrict__ start, const unsigned* __restrict__ keys,
     const unsigned* __restrict__ vals, const float2* __restrict__ geo,
     const float* __restrict__ sg, int C, int ncell, float* __restrict__ acc,
     float* __restrict__ carry_head, float* __restrict__ carry_tail, int* __restrict__ flags,
     const int* __restrict__ trow) {
+  using VF = VecF<V>;
+  typedef typename VF::T vt;
   const int lane = threadIdx.x & 63;
   const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = start[ncell];  // valid taps (sorted to the front)
   const int j0 = seg * 64;
   if (j0 >= n) return;
   const int jn = min(64, n - j0);
-  const int c = blockIdx.y * 64 + lane;
-  const bool cok = c < C;
+  const int c = (blockIdx.y * 64 + lane) * V;
+  const bool cok = c < C;  // (V = 4: C % 4 == 0)
   unsigned kl = 0xffffffffu, vl = 0;
   float2 gl = make_float2(0.f, 0.f);
   int tl = -1;
@@ -372,33 +407,32 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
   const unsigned knext = j0 + jn < n ? keys[j0 + jn] : 0xffffffffu;
   unsigned cur = __builtin_amdgcn_readfirstlane(kl);
   int runs = 0;
-  float a = 0.f;
+  vt a = VF::zero();
   auto flush = [&](bool last) {
     const bool cont_prev = runs == 0 && cur == kprev;
     const bool cont_next = last && cur == knext;
     if (cok) {
-      if (cont_prev) carry_head[(size_t)seg * C + c] = a;
-      else if (cont_next) carry_tail[(size_t)seg * C + c] = a;
-      else acc[(size_t)cur * C + c] = a;
+      if (cont_prev) VF::store(carry_head + (size_t)seg * C + c, a);
+      else if (cont_next) VF::store(carry_tail + (size_t)seg * C + c, a);
+      else VF::store(acc + (size_t)cur * C + c, a);
     }
     if (last && blockIdx.y == 0 && lane == 0)
       flags[seg] = (cont_next && !cont_prev ? 1 : 0) | (runs == 0 && cont_prev && cont_next ? 2 : 0);
     ++runs;
   };
   for (int j = 0; j < jn; j += 16) {
-    float sv[16];
+    vt sv[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {  // 16 sg rows in flight
+    for (int u = 0; u < 16; ++u) {  // 16 rows in flight
       if constexpr (S2) {
         // (a sample past the last selected bin — the last row / column of an even bin count —
         // keeps its taps with value 0, so the taps and their segments are those of the
-        // zero-padded 7 x 7 backward: the same sums in the same association; the bin row of
-        // each sample comes from rbg_geom_kernel, so no per-tap index arithmetic here)
+        // zero-padded 7 x 7 backward: the same sums in the same association)
         const int tr = __builtin_amdgcn_readlane(tl, min(j + u, jn - 1));
-        sv[u] = cok && tr >= 0 ? sg[(size_t)tr * C + c] * 0.25f : 0.f;  // = top / 4.f
+        sv[u] = cok && tr >= 0 ? vscale(VF::load(sg + (size_t)tr * C + c), 0.25f) : VF::zero();  // = top / 4.f
       } else {
         const unsigned vu = __builtin_amdgcn_readlane(vl, min(j + u, jn - 1));
-        sv[u] = cok ? sg[(size_t)(vu >> 2) * C + c] : 0.f;
+        sv[u] = cok ? VF::load(sg + (size_t)(vu >> 2) * C + c) : VF::zero();
       }
     }
 #pragma unroll
@@ -408,12 +442,12 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
       if (ku != cur) {
         flush(false);
         cur = ku;
-        a = 0.f;
+        a = VF::zero();
       }
       const unsigned vu = __builtin_amdgcn_readlane(vl, j + u);
       const float hr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl.x), j + u));
       const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gl.y), j + u));
-      a += tap_value(sv[u], hr, wr, (int)(vu & 3));
+      vtap(a, sv[u], hr, wr, (int)(vu & 3));
     }
   }
   flush(true);
@@ -745,9 +779,14 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     TLOD_LAUNCH_CHECK();
     TLOD_HIP(hipMemsetAsync(w.acc, 0, ncell_sz * C * sizeof(float), s));
     const int nseg = div_up(n, 64);
-    hipLaunchKernelGGL(rbg_seg_gather_kernel<false>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256),
-                       0, s, w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell, w.acc,
-                       w.carry_head, w.carry_tail, w.flags, (const int*)nullptr);
+    if (C % 4 == 0)
+      hipLaunchKernelGGL((rbg_seg_gather_kernel<false, 4>), dim3(div_up(nseg, 4), div_up(C, 256)),
+                         dim3(256), 0, s, w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell,
+                         w.acc, w.carry_head, w.carry_tail, w.flags, (const int*)nullptr);
+    else
+      hipLaunchKernelGGL((rbg_seg_gather_kernel<false, 1>), dim3(div_up(nseg, 4), div_up(C, 64)),
+                         dim3(256), 0, s, w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell,
+                         w.acc, w.carry_head, w.carry_tail, w.flags, (const int*)nullptr);
     TLOD_LAUNCH_CHECK();
     hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
                        w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
@@ -842,9 +881,14 @@ extern "C" int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, 
   TLOD_LAUNCH_CHECK();
   TLOD_HIP(hipMemsetAsync(w.acc, 0, (size_t)ncell * C * sizeof(float), s));
   const int nseg = div_up(n, 64);
-  hipLaunchKernelGGL(rbg_seg_gather_kernel<true>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0,
-                     s, w.start, w.keys_s, w.vals_s, w.geo, top_grad, C, (int)ncell, w.acc,
-                     w.carry_head, w.carry_tail, w.flags, w.trow);
+  if (C % 4 == 0)
+    hipLaunchKernelGGL((rbg_seg_gather_kernel<true, 4>), dim3(div_up(nseg, 4), div_up(C, 256)),
+                       dim3(256), 0, s, w.start, w.keys_s, w.vals_s, w.geo, top_grad, C, (int)ncell,
+                       w.acc, w.carry_head, w.carry_tail, w.flags, w.trow);
+  else
+    hipLaunchKernelGGL((rbg_seg_gather_kernel<true, 1>), dim3(div_up(nseg, 4), div_up(C, 64)),
+                       dim3(256), 0, s, w.start, w.keys_s, w.vals_s, w.geo, top_grad, C, (int)ncell,
+                       w.acc, w.carry_head, w.carry_tail, w.flags, w.trow);
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
                      w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
