@@ -367,6 +367,10 @@ __device__ __forceinline__ float vscale(float v, float s) { return v * s; }
 __device__ __forceinline__ float4 vscale(float4 v, float s) {
   return make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
 }
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 __device__ __forceinline__ void vtap(float& a, float g, float hr, float wr, int k) {
   a += tap_value(g, hr, wr, k);
 }
@@ -454,16 +458,19 @@ __global__ void __launch_bounds__(256) rbg_seg_gather_kernel(
 }
 
 // the runs crossing segments: the owning segment's tail piece, then the next segments' head
-// pieces in order (deterministic)
+// pieces in order (deterministic); V channels per lane as in the gather
+template <int V>
 __global__ void __launch_bounds__(256) rbg_seg_fixup_kernel(
     const int* __restrict__ start, const unsigned* __restrict__ keys, int C, int ncell,
     const float* __restrict__ carry_head, const float* __restrict__ carry_tail,
     const int* __restrict__ flags, float* __restrict__ acc) {
+  using VF = VecF<V>;
+  typedef typename VF::T vt;
   const int lane = threadIdx.x & 63;
   const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = start[ncell];
   if (seg * 64 >= n || !(flags[seg] & 1)) return;
-  const int c = blockIdx.y * 64 + lane;
+  const int c = (blockIdx.y * 64 + lane) * V;
   const unsigned cell = keys[min(seg * 64 + 64, n) - 1];
   // the run ends in the first later segment not flagged 2: found 64 flags at a time by the
   // lanes (a cell under hundreds of RoIs spans hundreds of segments), then its head pieces
@@ -480,17 +487,17 @@ __global__ void __launch_bounds__(256) rbg_seg_fixup_kernel(
   }
   if (kend * 64 >= n) --kend;
   if (c >= C) return;
-  float a = carry_tail[(size_t)seg * C + c];
+  vt a = VF::load(carry_tail + (size_t)seg * C + c);
   int k = seg + 1;
   for (; k + 8 <= kend + 1; k += 8) {
-    float h[8];
+    vt h[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) h[u] = carry_head[(size_t)(k + u) * C + c];
+    for (int u = 0; u < 8; ++u) h[u] = VF::load(carry_head + (size_t)(k + u) * C + c);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a += h[u];
+    for (int u = 0; u < 8; ++u) a = vadd(a, h[u]);
   }
-  for (; k <= kend; ++k) a += carry_head[(size_t)k * C + c];
-  acc[(size_t)cell * C + c] = a;
+  for (; k <= kend; ++k) a = vadd(a, VF::load(carry_head + (size_t)k * C + c));
+  VF::store(acc + (size_t)cell * C + c, a);
 }
 
 struct RbgWs {
@@ -583,25 +590,14 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restri
   }
 }
 
-// align_sample on a channels-last map (row pitch W * C, column pitch C)
-__device__ __forceinline__ float align_sample_nhwc(const float* __restrict__ base, int W, int C,
-                                                   int y, int x, float hr, float wr) {
-  const float* p = base + ((size_t)y * W + x) * C;
-  const float ul = p[0], ur = p[C];
-  const float dl = p[(size_t)W * C], dr = p[(size_t)W * C + C];
-  double t1 = ((double)ul * (1. - (double)hr)) * (1. - (double)wr);
-  double t2 = ((double)ur * (1. - (double)hr)) * (double)wr;
-  double t3 = (double)(dl * hr) * (1. - (double)wr);
-  double t4 = (double)((dr * hr) * wr);
-  return (float)(((t1 + t2) + t3) + t4);
-}
-
-// grid (R, ceil(C / 256)): thread = channel; out (R, QH, QW, C)
+// grid (R, ceil(C / (256 V))): thread = V consecutive channels (16-B loads for V = 4, each
+// channel's arithmetic unchanged); out (R, QH, QW, C)
+template <int V>
 __global__ void __launch_bounds__(256) roi_align_avg_s2_fwd_kernel(
     const float* __restrict__ feat_nhwc, float scale, int C, int H, int W, int ph, int pw,
     const float* __restrict__ rois, float* __restrict__ out) {
   const int ah = ph + 1, aw = pw + 1, QH = (ph + 1) / 2, QW = (pw + 1) / 2;
-  const int r = blockIdx.x, t = threadIdx.x, c = blockIdx.y * 256 + t;
+  const int r = blockIdx.x, t = threadIdx.x, c = (blockIdx.y * 256 + t) * V;
   __shared__ int gy[8], gx[8];
   __shared__ float ghr[8], gwr[8];
   __shared__ bool gvy[8], gvx[8];
@@ -617,20 +613,53 @@ __global__ void __launch_bounds__(256) roi_align_avg_s2_fwd_kernel(
   float* o = out + (size_t)r * QH * QW * C + c;
   for (int i = 0; i < QH; ++i)
     for (int j = 0; j < QW; ++j) {
-      float sv[4];
+      float sv[4][V];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int sy = 2 * i + (k >> 1), sx = 2 * j + (k & 1);
-        sv[k] = gvy[sy] && gvx[sx] ? align_sample_nhwc(base, W, C, gy[sy], gx[sx], ghr[sy], gwr[sx])
-                                   : 0.f;
+        if (gvy[sy] && gvx[sx]) {
+          const float* p = base + ((size_t)gy[sy] * W + gx[sx]) * C;
+          float ul[V], ur[V], dl[V], dr[V];
+          if constexpr (V == 4) {
+            const float4 a = *reinterpret_cast<const float4*>(p);
+            const float4 b = *reinterpret_cast<const float4*>(p + C);
+            const float4 d = *reinterpret_cast<const float4*>(p + (size_t)W * C);
+            const float4 e = *reinterpret_cast<const float4*>(p + (size_t)W * C + C);
+            ul[0] = a.x; ul[1] = a.y; ul[2] = a.z; ul[3] = a.w;
+            ur[0] = b.x; ur[1] = b.y; ur[2] = b.z; ur[3] = b.w;
+            dl[0] = d.x; dl[1] = d.y; dl[2] = d.z; dl[3] = d.w;
+            dr[0] = e.x; dr[1] = e.y; dr[2] = e.z; dr[3] = e.w;
+          } else {
+            ul[0] = p[0]; ur[0] = p[C]; dl[0] = p[(size_t)W * C]; dr[0] = p[(size_t)W * C + C];
+          }
+          const float hr = ghr[sy], wr = gwr[sx];
+#pragma unroll
+          for (int v = 0; v < V; ++v) {  // (align_sample's arithmetic on the channels-last map)
+            const double t1 = ((double)ul[v] * (1. - (double)hr)) * (1. - (double)wr);
+            const double t2 = ((double)ur[v] * (1. - (double)hr)) * (double)wr;
+            const double t3 = (double)(dl[v] * hr) * (1. - (double)wr);
+            const double t4 = (double)((dr[v] * hr) * wr);
+            sv[k][v] = (float)(((t1 + t2) + t3) + t4);
+          }
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) sv[k][v] = 0.f;
+        }
       }
       // avg_pool2d(2, s1) as roi_align_avg_fwd_kernel: ((((0+a)+b)+c)+d)/4
-      float acc = 0.f;
-      acc += sv[0];
-      acc += sv[1];
-      acc += sv[2];
-      acc += sv[3];
-      o[(size_t)(i * QW + j) * C] = acc / 4.f;
+      float res[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float acc = 0.f;
+        acc += sv[0][v];
+        acc += sv[1][v];
+        acc += sv[2][v];
+        acc += sv[3][v];
+        res[v] = acc / 4.f;
+      }
+      float* q = o + (size_t)(i * QW + j) * C;
+      if constexpr (V == 4) *reinterpret_cast<float4*>(q) = make_float4(res[0], res[1], res[2], res[3]);
+      else q[0] = res[0];
     }
 }
 
@@ -788,8 +817,14 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
                          dim3(256), 0, s, w.start, w.keys_s, w.vals_s, w.geo, w.sg, C, (int)ncell,
                          w.acc, w.carry_head, w.carry_tail, w.flags, (const int*)nullptr);
     TLOD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
-                       w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
+    if (C % 4 == 0)
+      hipLaunchKernelGGL(rbg_seg_fixup_kernel<4>, dim3(div_up(nseg, 4), div_up(C, 256)), dim3(256),
+                         0, s, w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail,
+                         w.flags, w.acc);
+    else
+      hipLaunchKernelGGL(rbg_seg_fixup_kernel<1>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256),
+                         0, s, w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail,
+                         w.flags, w.acc);
     TLOD_LAUNCH_CHECK();
     hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
                        0, s, w.acc, C, H * W, bottom_grad);
@@ -845,8 +880,12 @@ extern "C" int tlod_roi_align_avg_s2_nhwc_fwd_f32(const float* feat, int B, int 
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256), 0,
                      s, feat, C, H * W, fn);
   TLOD_LAUNCH_CHECK();
-  hipLaunchKernelGGL(roi_align_avg_s2_fwd_kernel, dim3(R, div_up(C, 256)), dim3(256), 0, s, fn,
-                     scale, C, H, W, ph, pw, rois, out);
+  if (C % 4 == 0)
+    hipLaunchKernelGGL(roi_align_avg_s2_fwd_kernel<4>, dim3(R, div_up(C, 1024)), dim3(256), 0, s, fn,
+                       scale, C, H, W, ph, pw, rois, out);
+  else
+    hipLaunchKernelGGL(roi_align_avg_s2_fwd_kernel<1>, dim3(R, div_up(C, 256)), dim3(256), 0, s, fn,
+                       scale, C, H, W, ph, pw, rois, out);
   TLOD_LAUNCH_CHECK();
   return kOk;
 }
@@ -890,8 +929,14 @@ extern "C" int tlod_roi_align_avg_s2_nhwc_bwd_f32(const float* top_grad, int B, 
                        dim3(256), 0, s, w.start, w.keys_s, w.vals_s, w.geo, top_grad, C, (int)ncell,
                        w.acc, w.carry_head, w.carry_tail, w.flags, w.trow);
   TLOD_LAUNCH_CHECK();
-  hipLaunchKernelGGL(rbg_seg_fixup_kernel, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0, s,
-                     w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags, w.acc);
+  if (C % 4 == 0)
+    hipLaunchKernelGGL(rbg_seg_fixup_kernel<4>, dim3(div_up(nseg, 4), div_up(C, 256)), dim3(256), 0,
+                       s, w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags,
+                       w.acc);
+  else
+    hipLaunchKernelGGL(rbg_seg_fixup_kernel<1>, dim3(div_up(nseg, 4), div_up(C, 64)), dim3(256), 0,
+                       s, w.start, w.keys_s, C, (int)ncell, w.carry_head, w.carry_tail, w.flags,
+                       w.acc);
   TLOD_LAUNCH_CHECK();
   hipLaunchKernelGGL(nhwc_add_to_nchw_kernel, dim3(div_up(H * W, 64), div_up(C, 64), B), dim3(256),
                      0, s, w.acc, C, H * W, bottom_grad);
