@@ -28,7 +28,7 @@ from .. import _lib
 from ..config import cfg
 from .. import conv as conv_mod
 from ..conv import ConvBNFunction, ShortcutLink
-from ..linear import LinearActFunction, LinearFunction, linear_math
+from ..linear import LinearActFunction, linear_math
 
 
 def fold_bn(bn):
@@ -197,11 +197,13 @@ class Bottleneck(nn.Module):
             if residual is not None:
                 y = y.add_(residual)
             return F.relu(y, inplace=True) if relu else y
-        if residual is None and not relu:
-            return LinearFunction.apply(xm.contiguous(), wm * scale[:, None], shift, m)
-        # residual add and ReLU in the GEMM epilogue (tlod_gemm_bs_ex_f32)
-        return LinearActFunction.apply(xm.contiguous(), wm * scale[:, None], shift, residual,
-                                       relu, m, relu_in, link, role)
+        # residual add and ReLU in the GEMM epilogue (tlod_gemm_bs_ex_f32); the folded weight
+        # is built outside autograd and the weight gradient written into the conv weight's
+        # slot by the GEMM function (wsrc / wscale)
+        with torch.no_grad():
+            wf = (wm * scale[:, None]).contiguous()
+        return LinearActFunction.apply(xm.contiguous(), wf, shift, residual, relu, m, relu_in,
+                                       link, role, w, scale)
 
     def forward_nhwc(self, x, subsampled=False, shape=None, relu_in=False):
         """The layer4 RoI head, channels-last.  x: (R, H, W, C), or (R*H*W, C) rows with

@@ -130,10 +130,16 @@ class LinearActFunction(torch.autograd.Function):
     (gemm_mask) and tagged, so that layer's backward skips its own mask pass (a gradient that
     arrives tagged for this y is already g).  link (a tlod.conv.ShortcutLink) / role: an
     identity bottleneck's conv3 (role 3) hands its residual gradient g to conv1 (role 1),
-    whose input gradient adds it in the same epilogue — no autograd sum of the two."""
+    whose input gradient adds it in the same epilogue — no autograd sum of the two.
+    wsrc / wscale (a conv weight (O, C, kh, kw) and a per-output scale): `weight` is the GEMM
+    form of wsrc * wscale (rows (kh, kw, c) for 3x3), computed by the caller without autograd;
+    the backward writes d wsrc = (dy^T x in the GEMM form) * wscale, re-laid out, straight
+    into wsrc's gradient slot (one pass) instead of autograd's mul, permute copy and the
+    arena's copy of the result."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, relu, math, relu_in=False, link=None, role=0):
+    def forward(ctx, x, weight, bias, residual, relu, math, relu_in=False, link=None, role=0,
+                wsrc=None, wscale=None):
         R, I = x.shape
         O = weight.shape[0]
         y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math, residual=residual, relu=relu)
@@ -141,6 +147,7 @@ class LinearActFunction(torch.autograd.Function):
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
         ctx.params = (weight, bias)
         ctx.relu_in, ctx.link, ctx.role = bool(relu_in), link, role
+        ctx.wsrc, ctx.wscale = wsrc, wscale
         ctx.save_for_backward(x, weight, y if relu else None)
         return y
 
@@ -168,13 +175,26 @@ class LinearActFunction(torch.autograd.Function):
                 dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math, residual=res)
         if ctx.needs_input_grad[1]:
             dw = gemm(g, x, O, I, R, 0, 0, None, ctx.math, out=grad_out(ctx.params[0]))
+        dsrc = None
+        if ctx.wsrc is not None and ctx.needs_input_grad[9]:
+            w = ctx.wsrc
+            dwg = gemm(g, x, O, I, R, 0, 0, None, ctx.math)  # (O, I) in the GEMM layout
+            slot = grad_out(w)
+            dsrc = slot if slot is not None else torch.empty_like(w)
+            sc = ctx.wscale.detach()
+            if w.shape[2] == 1:
+                torch.mul(dwg, sc[:, None], out=dsrc.view(O, -1))
+            else:  # rows (kh, kw, c) -> (c, kh, kw)
+                kh, kw = w.shape[2], w.shape[3]
+                torch.mul(dwg.view(O, kh, kw, -1).permute(0, 3, 1, 2), sc.view(-1, 1, 1, 1),
+                          out=dsrc)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             slot = grad_out(ctx.params[1])
             db = g.sum(0) if slot is None else torch.sum(g, 0, out=slot)
         dres = g if ctx.has_res and ctx.needs_input_grad[3] else None
         if dres is not None and ctx.role == 3 and ctx.link is not None:
             ctx.link.g, dres = dres, None  # to conv1's backward
-        return dx, dw, db, dres, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, dsrc, None
 
 
 class Linear(nn.Linear):
