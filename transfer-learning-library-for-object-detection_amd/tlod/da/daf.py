@@ -29,6 +29,7 @@ from ..roi_pool import _RoIPooling
 from ..rpn.proposal import proposals_on_side_streams
 from ..rpn.proposal_target import _ProposalTargetLayer
 from ..rpn.rpn_head import _RPN
+from ..detector import resnet as _resnet_mod
 
 
 class GRLayer(torch.autograd.Function):
@@ -346,4 +347,4 @@ class resnet(_fasterRCNN):
 
     def _head_to_tail(self, pool5):
         # RCNN_top(pool5).mean(3).mean(2) (resnet.py:286-288); the head runs channels-last
-        return self.RCNN_top(pool5).mean(2).mean(1)
+        return _resnet_mod.head_mean(self.RCNN_top(pool5))

@@ -302,6 +302,28 @@ class ResNetTop(nn.Sequential):
         return x.view(*shape, x.shape[-1])
 
 
+class HeadMeanFunction(torch.autograd.Function):
+    """fc7 = RCNN_top(pool5).mean(3).mean(2) (lib/DAF/resnet.py:286-288) on the channels-last
+    head output (R, H, W, C): the same two means forward; the backward returns (g / H) / W
+    (the order of autograd's two mean backwards) broadcast as a stride-0 view — autograd's chain materialises it twice (one (R, H, C) and
+    one (R, H, W, C) division) before the last bottleneck's ReLU mask reads it, which takes
+    the view directly (LinearActFunction)."""
+
+    @staticmethod
+    def forward(ctx, y):
+        ctx.shape = y.shape
+        return y.mean(2).mean(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        R, H, W, C = ctx.shape
+        return ((g / H) / W)[:, None, None, :].expand(R, H, W, C)
+
+
+def head_mean(y):
+    return HeadMeanFunction.apply(y)
+
+
 def _make_layer(inplanes, planes, blocks, stride=1):
     downsample = None
     if stride != 1 or inplanes != planes * 4:
