@@ -131,9 +131,14 @@ __global__ void im2col3x3_nhwc_kernel(const float4* __restrict__ x, int H, int W
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int hh = h + t / 3 - 1, ww = w + t % 3 - 1;
-      o[(size_t)t * C4] = (hh >= 0 && hh < H && ww >= 0 && ww < W)
-                              ? x[((r * H + hh) * W + ww) * C4 + c]
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v = (hh >= 0 && hh < H && ww >= 0 && ww < W)
+                           ? x[((r * H + hh) * W + ww) * C4 + c]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      // streaming store: the 9x tap matrix (GBs on ATF's thousands of RoIs) does not fit
+      // the caches, so it bypasses them (nontemporal)
+      typedef float v4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(v4{v.x, v.y, v.z, v.w},
+                                  reinterpret_cast<v4*>(o + (size_t)t * C4));
     }
   }
 }
@@ -152,7 +157,10 @@ __global__ void col2im3x3_nhwc_kernel(const float4* __restrict__ col, int H, int
     for (int t = 0; t < 9; ++t) {  // output pixel (h - kh + 1, w - kw + 1) took x(h, w) as tap t
       const int oh = h - t / 3 + 1, ow = w - t % 3 + 1;
       if (oh >= 0 && oh < H && ow >= 0 && ow < W) {
-        const float4 v = col[(((r * H + oh) * W + ow) * 9 + t) * C4 + c];
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        const v4 vv = __builtin_nontemporal_load(
+            reinterpret_cast<const v4*>(col + (((r * H + oh) * W + ow) * 9 + t) * C4 + c));
+        const float4 v = make_float4(vv.x, vv.y, vv.z, vv.w);
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
     }
