@@ -13,19 +13,15 @@
  *     launchers do: roi_align_kernel.cu:84-88);
  *   - tensors are contiguous NCHW float32 (the reference's layout and dtype).
  *
- * Environment switches (read ONCE per process, at the first call that consults them; they
- * choose between kernels that compute the same result — none is needed for correctness):
+ * Environment switches (they choose between kernels that compute the same result — none is
+ * needed for correctness):
  *   TLOD_ROI_BWD_GATHER=0  RoIAlignAvg backward on the atomic kernels instead of the
  *                          deterministic sorted-tap gather (the gather workspace query then
- *                          returns 0);
- *   TLOD_WGRAD_WS=0        3x3 bf16x6 weight gradient on the im2col kernel instead of the
- *                          warp-specialized pixel-tile kernel;
- *   TLOD_WG1X1_TILE=256|128  1x1 split-bf16 weight gradient tile (default: cost model);
- *   TLOD_CONV_KSPLIT_MAX=n, TLOD_WGWS_SPLIT_MAX=n  caps on the split-K planners (A/B only);
- *   TLOD_CONV_WS=0, TLOD_WS_MINCIN=n, TLOD_WS_FLEX=0, TLOD_CONV_BAND=0,
- *   TLOD_CONV_FWD_CK=4, TLOD_CONV_WGRAD_TH=2
- *                          split-bf16 / f32 conv forward tilings (see csrc/conv.hip);
- * the workspace queries follow the same switches, so query after setting them.
+ *                          returns 0; read at every call, so set it before the query);
+ *   TLOD_CU_RESERVE=n      initial value of tlod_set_cu_reserve (CUs the planners leave out);
+ * the workspace queries follow the same switches, so query after setting them.  The conv
+ * planners' tiling / split A/B switches (TLOD_CONV_WS, TLOD_WS_FLEX, TLOD_CONV_KSPLIT_MAX,
+ * TLOD_WGRAD_WS, ...) are compile-time defines in csrc/*.hip, not run-time switches.
  *
  * Each entry point names the reference interface it replaces (paths relative to the
  * reference checkout).

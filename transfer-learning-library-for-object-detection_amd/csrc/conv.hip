@@ -54,6 +54,28 @@ namespace tlod {
 #ifndef TLOD_CONV_OCC
 #define TLOD_CONV_OCC __attribute__((amdgpu_waves_per_eu(2, 4)))
 #endif
+// Planner / kernel-selection A/B switches, compile time only (rebuild with -D to measure a
+// variant; the shipped library holds no run-time variant paths).  Defaults are the measured
+// choices: split caps (profiles/r04/split_caps_sweep.txt), the warp-specialized kernel and
+// its flexible tiles, band tiles for padded narrow maps.
+#ifndef TLOD_CONV_KSPLIT_MAX  // cap of the forward / dgrad K split
+#define TLOD_CONV_KSPLIT_MAX 8
+#endif
+#ifndef TLOD_CONV_BAND  // 0: no band tiles
+#define TLOD_CONV_BAND 1
+#endif
+#ifndef TLOD_CONV_WS  // 0: no warp-specialized forward / dgrad kernel
+#define TLOD_CONV_WS 1
+#endif
+#ifndef TLOD_WS_MINCIN  // smallest Cin on the warp-specialized kernel
+#define TLOD_WS_MINCIN 128
+#endif
+#ifndef TLOD_WS_FLEX  // 0: warp-specialized tiles fixed at 16 x 32
+#define TLOD_WS_FLEX 1
+#endif
+#ifndef TLOD_WG1X1_TILE  // 1x1 wgrad tile: 0 = cost model, 256 / 128 = forced
+#define TLOD_WG1X1_TILE 0
+#endif
 
 // Out-of-range staging loads read this zero block instead of branching (a branch per
 // load makes hipcc wait vmcnt(0) after each one; a select after the load pins the wait
@@ -1927,11 +1949,6 @@ __global__ void __launch_bounds__(kReluThreads) relu_bwd_bias_kernel(
 }
 
 // ======================================================================= launchers
-// Tile-variant knobs for A/B measurement (read once; defaults are the tuned choices).
-static int tune_knob(const char* name, int def) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : def;
-}
 
 struct FwdPlan {
   int tiles_m, tiles_w, tiles_h;
@@ -1968,8 +1985,7 @@ static FwdPlan plan_schedule(int tiles_m, int tiles_w, int tiles_h, int N, int n
   if (!allow_split) return p;
   const double tile_s = tile_flops / (157.3e12 * 0.65 / slots);
   double best = (double)((T + slots - 1) / slots) * tile_s;
-  static const int kcap = tune_knob("TLOD_CONV_KSPLIT_MAX", 8);  // A/B: cap the K split
-  const int kmax = std::min({8, kcap, nchunks / 2});
+  const int kmax = std::min({8, TLOD_CONV_KSPLIT_MAX, nchunks / 2});
   const long long q = T / slots;
   for (int k = 2; k <= kmax; ++k) {
     const int cps = div_up(div_up(nchunks, k), cps_align) * cps_align;
@@ -2057,7 +2073,6 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, Epi epi, float* Y,
   } while (0)
   if (KS == 3) {
     if (Cout <= 64) TLOD_FWD_CFG(1, 8, 2, 2, 8, 3);
-    if (tune_knob("TLOD_CONV_FWD_CK", 8) == 4) TLOD_FWD_CFG(2, 4, 2, 2, 4, 3);
     TLOD_FWD_CFG(2, 4, 2, 2, 8, 3);
   }
   if (KS == 1) {
@@ -2073,7 +2088,7 @@ static int conv_fwd_dispatch(const float* X, const float* Wk, Epi epi, float* Y,
 // Band tiles pay off where 32-wide column tiles pad the map badly (conv5 / RPN at 37x75:
 // 40% padding; 75x150: 6%), and fit the staged patch only for narrow maps.
 static bool use_band(int H, int W) {
-  if (!band_fits(W) || tune_knob("TLOD_CONV_BAND", 1) == 0) return false;
+  if (!band_fits(W) || TLOD_CONV_BAND == 0) return false;
   const double util2d = (double)H * W / ((double)div_up(H, 16) * 16 * div_up(W, 32) * 32);
   const double utilb = (double)H * W / ((double)div_up(H * W, 512) * 512);
   return utilb > util2d * 1.05;
@@ -2082,26 +2097,22 @@ static bool use_band(int H, int W) {
 // Warp-specialized forward kernel (conv_fwd_bs_ws_kernel) instead of conv_fwd_bs_kernel.
 // Warp-specialized forward for 2D tiles with >= 16 input-channel chunks (Cin >= 128):
 // measured 5-8% faster on conv3/conv4 fwd and dgrad, ~2% slower at Cin = 64 (4 chunk pairs
-// per tile: the per-tile prologue dominates).  TLOD_CONV_WS=0 disables it.
+// per tile: the per-tile prologue dominates).
 // One predicate for the plan (resident slots) and the launch.
 static bool use_ws(int Cin, int Cout, int H, int W) {
-  static const bool ws = tune_knob("TLOD_CONV_WS", 1) != 0;
-  static const int min_cin = tune_knob("TLOD_WS_MINCIN", 128);
   // raw buffer loads / stores: 32-bit byte offsets into one image (+ 8 channels of headroom)
-  return ws && Cin >= min_cin && (size_t)(std::max(Cin, Cout) + 8) * H * W * 4 < (1ull << 31);
+  return TLOD_CONV_WS != 0 && Cin >= TLOD_WS_MINCIN && (size_t)(std::max(Cin, Cout) + 8) * H * W * 4 < (1ull << 31);
 }
 
 // Tile of the warp-specialized kernel for an H x W map: the fewest tiles of TH x TW <= 512
 // pixels whose patch fits the staging (real (TH + 2) x (TW + 2) <= kWsPos positions, staged
 // (TH + 2) x ws_pitch(TW) <= kWsAlloc); ties go to the smaller halo (patch / pixels, to
-// 0.05), then the wider tile (coalesced staging rows).  Pooling epilogues and
-// TLOD_WS_FLEX=0 keep 16 x 32.
+// 0.05), then the wider tile (coalesced staging rows).  Pooling epilogues keep 16 x 32.
 struct WsTile {
   int th, tw;
 };
 static WsTile ws_tile(int H, int W, bool pool) {
-  static const bool flex = tune_knob("TLOD_WS_FLEX", 1) != 0;
-  if (pool || !flex) return {16, 32};
+  if (pool || TLOD_WS_FLEX == 0) return {16, 32};
   WsTile best{16, 32};
   long long best_t = (long long)div_up(H, 16) * div_up(W, 32);
   int best_h = 24;  // halo of 16 x 32 (612 / 512 = 1.195) in units of 0.05
@@ -2225,7 +2236,7 @@ static int conv_fwd_bs_dispatch(const float* X, const unsigned short* Wp, Epi ep
   } while (0)
   // pooling: 2D tiles; the warp-specialized kernel's flexible tiles replace band tiles
   const bool band = use_band(H, W) && epi.pool == nullptr &&
-                    !(use_ws(Cin, Cout, H, W) && tune_knob("TLOD_WS_FLEX", 1) != 0);
+                    !(use_ws(Cin, Cout, H, W) && TLOD_WS_FLEX != 0);
   if (nprod == 6 && band) TLOD_BS_CFG(1, 8, 2, 2, 6, true);
   if (nprod == 6) TLOD_BS_CFG(1, 8, 2, 2, 6, false);
   if (band) TLOD_BS_CFG(1, 8, 2, 2, 3, true);
@@ -2277,12 +2288,10 @@ struct Wgrad {
   }
 };
 
-// The wgrad tile config per kernel size (TLOD_CONV_WGRAD_TH=2 selects the 2-row variant).
+// The wgrad tile config per kernel size.
 template <typename F>
 static int with_wgrad_cfg(int KS, F&& f) {
-  static const int th = tune_knob("TLOD_CONV_WGRAD_TH", 1) == 2 ? 2 : 1;
-  if (KS == 3 && th == 1) return f(Wgrad<2, 4, 2, 2, 3, 1>{});
-  if (KS == 3) return f(Wgrad<2, 4, 2, 2, 3, 2>{});
+  if (KS == 3) return f(Wgrad<2, 4, 2, 2, 3, 1>{});
   if (KS == 1) return f(Wgrad<2, 2, 2, 2, 1, 2>{});
   return -1;
 }
@@ -2347,14 +2356,10 @@ struct WgradBs {
 // 256 x 256 tiles leave a handful of tiles that must be split many ways over the pixels, each
 // split writing a full dW slab: 256 -> 1024 at 38x75 ran 4 tiles x 64 splits (64 MB of
 // slabs).  128 x 128 tiles give 4x the tiles for 1/4 of the slab traffic at a lower MFMA
-// efficiency; the cost model picks (TLOD_WG1X1_TILE = 256 / 128 forces one).
+// efficiency; the cost model picks.
 static bool wgrad1x1_small_tile(int N, int Cin, int H, int W, int Cout, int nprod) {
-  static const int force = [] {
-    const char* e = getenv("TLOD_WG1X1_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  if (force == 256) return false;
-  if (force == 128) return true;
+  if (TLOD_WG1X1_TILE == 256) return false;
+  if (TLOD_WG1X1_TILE == 128) return true;
   double t_big = 0, t_small = 0;
   if (nprod == 6) {
     WgradBs<2, 4, 4, 2, 1, 6>::splits(N, Cin, H, W, Cout, &t_big);

@@ -757,14 +757,11 @@ extern "C" size_t tlod_roi_align_avg_bwd_workspace_bytes(int B, int C, int H, in
   return (size_t)B * C * H * W * sizeof(float);
 }
 
-// The sorted-tap gather backward is the default; TLOD_ROI_BWD_GATHER=0 (read once per process,
+// The sorted-tap gather backward is the default; TLOD_ROI_BWD_GATHER=0 (read at every call,
 // documented in tlod.h) selects the atomic kernels, and then the gather needs no workspace.
 static bool roi_bwd_gather_on() {
-  static const bool on = [] {
-    const char* v = getenv("TLOD_ROI_BWD_GATHER");
-    return !(v && *v == '0');
-  }();
-  return on;
+  const char* v = getenv("TLOD_ROI_BWD_GATHER");
+  return !(v && *v == '0');
 }
 
 extern "C" size_t tlod_roi_align_avg_bwd_gather_workspace_bytes(int B, int C, int H, int W, int R,

@@ -67,6 +67,12 @@ static_assert(A_ITEMS % (NPW * 64) == 0, "A staging");
 #ifndef TLOD_WGWS_BSPLIT  // 1: the MFMA waves stage B (the X patch), the producers only A
 #define TLOD_WGWS_BSPLIT 1
 #endif
+#ifndef TLOD_WGRAD_WS  // A/B: 0 keeps every 3x3 bf16x6 wgrad on conv_wgrad_bs_kernel
+#define TLOD_WGRAD_WS 1
+#endif
+#ifndef TLOD_WGWS_SPLIT_MAX  // A/B: cap of the split count (profiles/r04/split_caps_sweep.txt)
+#define TLOD_WGWS_SPLIT_MAX 256
+#endif
 #ifndef TLOD_WGWS_KSUM  // per-k-step sums of the cross products (accuracy; see the k-step)
 #define TLOD_WGWS_KSUM 0
 #endif
@@ -547,13 +553,9 @@ __global__ void __launch_bounds__(256) wgws_reduce_kernel(const float* __restric
 
 // Every 3x3 bf16x6 weight gradient (any channel counts and map sizes: ragged channel octets,
 // pixel tiles past the map and rows past Cout are masked) whose tensors fit 32-bit buffer
-// offsets.  TLOD_WGRAD_WS=0 keeps the im2col kernel (conv_wgrad_bs_kernel).
+// offsets (compile with -DTLOD_WGRAD_WS=0 to keep the im2col kernel, conv_wgrad_bs_kernel).
 bool wgrad_ws_applies(int N, int Cin, int H, int W, int Cout, int KS, int nprod) {
-  static const bool on = [] {
-    const char* v = getenv("TLOD_WGRAD_WS");
-    return !(v && *v && atoi(v) == 0);
-  }();
-  return on && KS == 3 && nprod == 6 &&
+  return TLOD_WGRAD_WS != 0 && KS == 3 && nprod == 6 &&
          (size_t)N * (std::max(Cin, Cout) + 8) * H * W * 4 < (1ull << 31);
 }
 
@@ -574,11 +576,7 @@ static WgwsPlan wgws_plan(int N, int Cin, int H, int W, int Cout) {
   const double tile_bytes = (double)TILE_FLOATS * 4.0;
   int best = 1;
   double best_t = 1e30;
-  static const int spcap = [] {  // A/B: cap the split count (TLOD_WGWS_SPLIT_MAX)
-    const char* v = getenv("TLOD_WGWS_SPLIT_MAX");
-    return v && *v ? std::max(1, atoi(v)) : 256;
-  }();
-  for (int sp = 1; sp <= std::min({256, spcap, chunks}); ++sp) {
+  for (int sp = 1; sp <= std::min({256, TLOD_WGWS_SPLIT_MAX, chunks}); ++sp) {
     const int cps = div_up(chunks, sp);
     const int esp = div_up(chunks, cps);
     const long long rounds = ((long long)tiles * esp + slots - 1) / slots;
