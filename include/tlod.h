@@ -21,7 +21,7 @@
  *   TLOD_CU_RESERVE=n      initial value of tlod_set_cu_reserve (CUs the planners leave out);
  * the workspace queries follow the same switches, so query after setting them.  The conv
  * planners' tiling / split A/B switches (TLOD_CONV_WS, TLOD_WS_FLEX, TLOD_CONV_KSPLIT_MAX,
- * TLOD_WGRAD_WS, ...) are compile-time defines in csrc/*.hip, not run-time switches.
+ * TLOD_WGRAD_WS, ...) are compile-time defines in the csrc .hip sources, not run-time switches.
  *
  * Each entry point names the reference interface it replaces (paths relative to the
  * reference checkout).
