@@ -26,6 +26,26 @@ def clustered_boxes(rng, n, W=1000, H=600, clusters=40):
     return np.clip(b, 0, [W - 1, H - 1, W - 1, H - 1]).astype(np.float32)
 
 
+def anchor_grid_boxes(rng, H=37, W=75, stride=16, imh=600, imw=1200, jitter=2.0):
+    """RPN-like proposals: the 9 anchors (scales 8/16/32, ratios 0.5/1/2) at every feature
+    cell of a 600x1200 image, slightly jittered and clipped (what the proposal layer's NMS
+    sees from a fresh RPN: dense, heavily overlapping, ~1 in 3 kept at IoU 0.7)."""
+    base = []
+    for r in (0.5, 1.0, 2.0):
+        for sc in (8, 16, 32):
+            w, h = 16 * sc / np.sqrt(r), 16 * sc * np.sqrt(r)
+            base.append([7.5 - 0.5 * (w - 1), 7.5 - 0.5 * (h - 1), 7.5 + 0.5 * (w - 1),
+                         7.5 + 0.5 * (h - 1)])
+    ys, xs = np.meshgrid(np.arange(H) * stride, np.arange(W) * stride, indexing="ij")
+    sh = np.stack([xs, ys, xs, ys], -1).reshape(-1, 1, 4)
+    b = (sh + np.array(base)[None]).reshape(-1, 4) + rng.normal(0, jitter, (H * W * 9, 4))
+    b[:, 0::2] = np.clip(b[:, 0::2], 0, imw - 1)
+    b[:, 1::2] = np.clip(b[:, 1::2], 0, imh - 1)
+    b[:, 2] = np.maximum(b[:, 2], b[:, 0])
+    b[:, 3] = np.maximum(b[:, 3], b[:, 1])
+    return b.astype(np.float32)
+
+
 def sorted_dets(boxes, rng):
     s = rng.permutation(len(boxes)).astype(np.float32) / max(len(boxes), 1)  # tie-free
     order = np.argsort(-s, kind="stable")

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import clustered_boxes, random_boxes, sorted_dets
+from helpers import anchor_grid_boxes, clustered_boxes, random_boxes, sorted_dets
 from oracle import nms as onms
 from oracle import roi as oroi
 
@@ -45,6 +45,15 @@ def test_nms_max_keep_and_duplicates():
     d = sorted_dets(b, rng)
     for mk in (1, 63, 64, 65, 300, 2000):
         np.testing.assert_array_equal(_nms(d, 0.7, mk), onms.nms(d, 0.7, max_keep=mk))
+
+
+@pytest.mark.parametrize("n,mk", [(12000, 2000), (6000, 300), (12000, 0), (4000, 65)])
+def test_nms_anchor_grid_proposals(n, mk):
+    """The proposal layer's regime (dense anchors, ~20-50 survivors per 64-box block, early
+    stop at post_nms): exercises the scan's survivor-row fetches across many blocks."""
+    rng = np.random.default_rng(n + mk)
+    d = sorted_dets(anchor_grid_boxes(rng), rng)[:n]
+    np.testing.assert_array_equal(_nms(d, 0.7, mk), onms.nms(d, 0.7, max_keep=mk or None))
 
 
 def test_nms_empty():
