@@ -396,6 +396,23 @@ int tlod_conv1x1_gemm_bs_ex_f32(const float* x, const float* w, int w_layout, co
                                 int Cout, int relu, int nprod, void* ws, size_t ws_bytes,
                                 tlod_stream_t stream);
 
+/* 1x1 convolutions with 1 <= Cout <= 4, NCHW f32 (stride 1): the image-level domain
+ * classifier's last layer, _ImageDA.Conv2 = nn.Conv2d(512, 2, 1, bias=False)
+ * (lib/DAF/DA.py:36-50; ATF: three of them, on layer1 / layer2 / layer3 maps,
+ * lib/ATF/faster_rcnn.py).  Streaming kernels, deterministic (fixed summation orders).
+ * fwd: y (N, Cout, H, W) = weight (Cout, Cin) . x (+ bias[Cout], may be NULL).
+ * dgrad: dx (N, Cin, H, W) = weight^T . dy (written, not accumulated).
+ * wgrad: dweight (Cout, Cin) and dbias (Cout, may be NULL) written (not accumulated);
+ * workspace from tlod_conv1x1_small_wgrad_workspace_bytes. */
+int tlod_conv1x1_small_fwd_f32(const float* x, int N, int Cin, int H, int W, const float* weight,
+                               const float* bias, int Cout, float* y, tlod_stream_t stream);
+int tlod_conv1x1_small_dgrad_f32(const float* dy, int N, int Cout, int H, int W,
+                                 const float* weight, int Cin, float* dx, tlod_stream_t stream);
+size_t tlod_conv1x1_small_wgrad_workspace_bytes(int N, int Cin, int H, int W, int Cout);
+int tlod_conv1x1_small_wgrad_f32(const float* dy, const float* x, int N, int Cin, int H, int W,
+                                 int Cout, float* dweight, float* dbias, void* ws,
+                                 size_t ws_bytes, tlod_stream_t stream);
+
 /* ------------------------------------------------------------------ Max pooling
  * Replaces: nn.MaxPool2d(kernel_size=2, stride=2) (floor mode) in RCNN_base (torchvision
  *   vgg16().features, lib/DAF/vgg16.py:49) and, backward, its routing fused with the

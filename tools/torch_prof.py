@@ -44,3 +44,15 @@ tot = sum(r[0] for r in rows)
 print(f"torch-side device time per step: {tot / 1e3:.2f} ms")
 for dt, n, k, fr in rows[:30]:
     print(f"{dt / 1e3:7.3f} ms {n:6.1f}x  {k[:50]:50s}  {' <- '.join(f.split('/tlod/')[-1] for f in fr)}")
+# the glue ops by input shape (their call sites: grep the shapes)
+print("-- by input shape: copy_ / mm / add_ / cat / elementwise")
+srows = []
+for e in prof.key_averages(group_by_input_shape=True):
+    dt = getattr(e, "self_device_time_total", 0) or getattr(e, "self_cuda_time_total", 0)
+    if dt <= 0 or e.key not in ("aten::copy_", "aten::mm", "aten::add_", "aten::cat", "aten::addmm",
+                                "aten::mul", "aten::fill_", "aten::zero_", "aten::sum"):
+        continue
+    srows.append((dt / steps, e.count / steps, e.key, str(e.input_shapes)[:110]))
+srows.sort(key=lambda r: -r[0])
+for dt, n, k, sh in srows[:40]:
+    print(f"{dt / 1e3:7.3f} ms {n:6.1f}x  {k:14s} {sh}")

@@ -131,6 +131,11 @@ SIGNATURES = {
                                          c_int, c_int, c_int, P, c_size_t, P]),
     "tlod_conv1x1_gemm_bs_ex_f32": (c_int, [P, P, c_int, P, P, P, P, P, P, c_int, c_int, c_int,
                                             c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "tlod_conv1x1_small_fwd_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P, c_int, P, P]),
+    "tlod_conv1x1_small_dgrad_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P]),
+    "tlod_conv1x1_small_wgrad_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "tlod_conv1x1_small_wgrad_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P, P,
+                                             c_size_t, P]),
     "tlod_maxpool2x2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_maxpool2x2_relu_bwd_f32": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),
     "tlod_conv_fwd_bs_pool_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -640,6 +640,61 @@ class ConvPoolFunction(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class Conv1x1SmallFunction(torch.autograd.Function):
+    """1x1 conv with 1 <= Cout <= 4 (no ReLU): _ImageDA.Conv2 (512 -> 2, lib/DAF/DA.py:36-50)
+    on the streaming kernels of csrc/conv_small.hip (tlod_conv1x1_small_{fwd,dgrad,wgrad}_f32)
+    instead of F.linear over a channels-last copy.  The weight gradient is written into its
+    arena slot when one is free (tlod.grads)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _lib.require_cuda(x, weight)
+        x = x.contiguous()
+        N, Cin, H, W = x.shape
+        Cout = weight.shape[0]
+        w = weight.detach().reshape(Cout, Cin).contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        y = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.lib().tlod_conv1x1_small_fwd_f32(
+            _lib.ptr(x), N, Cin, H, W, _lib.ptr(w), _lib.ptr(b), Cout, _lib.ptr(y),
+            _lib.stream_of(x)), "conv1x1_small_fwd")
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        weight, bias = ctx.params
+        dy = dy.contiguous()
+        N, Cin, H, W = x.shape
+        Cout = w.shape[0]
+        L = _lib.lib()
+        st = _lib.stream_of(dy)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _lib.check(L.tlod_conv1x1_small_dgrad_f32(_lib.ptr(dy), N, Cout, H, W, _lib.ptr(w),
+                                                      Cin, _lib.ptr(dx), st), "conv1x1_small_dgrad")
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or need_b:
+            dw = grad_out(weight) if ctx.needs_input_grad[1] else None
+            if dw is None:
+                dw = torch.empty_like(weight)
+            if need_b:
+                db = grad_out(bias)
+                if db is None:
+                    db = torch.empty_like(bias)
+            ws = _lib.workspace(L.tlod_conv1x1_small_wgrad_workspace_bytes(N, Cin, H, W, Cout),
+                                dy.device, "conv1x1_small")
+            _lib.check(L.tlod_conv1x1_small_wgrad_f32(
+                _lib.ptr(dy), _lib.ptr(x), N, Cin, H, W, Cout, _lib.ptr(dw), _lib.ptr(db),
+                _lib.ptr(ws), ws.numel(), st), "conv1x1_small_wgrad")
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db
+
+
 class Conv2d(nn.Conv2d):
     """nn.Conv2d-compatible (stride 1, padding k//2) with the libtlod kernels; optional
     fused ReLU."""
@@ -664,8 +719,10 @@ class Conv2d(nn.Conv2d):
             if not needs_grad:
                 return conv_fwd_pool(x, self.weight, self.bias)
             return ConvPoolFunction.apply(x, self.weight, self.bias, self.act_tap)
+        if self.out_channels <= 4 and self.kernel_size[0] == 1 and not self.relu:
+            return Conv1x1SmallFunction.apply(x, self.weight, self.bias)
         if self.out_channels % 4:
-            # GEMM-library path for the tiny 1x1 heads (e.g. 512->2 of _ImageDA.Conv2)
+            # GEMM-library path for other odd-width 1x1 heads
             assert self.kernel_size[0] == 1
             y = F.linear(x.permute(0, 2, 3, 1), self.weight.view(self.out_channels, -1), self.bias)
             y = y.permute(0, 3, 1, 2).contiguous()
