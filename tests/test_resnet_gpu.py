@@ -193,6 +193,41 @@ def test_head_fused_backward_bit_identical(R, entry, monkeypatch):
         assert torch.equal(a, b), i
 
 
+@pytest.mark.parametrize("entry", [True, False])
+def test_head_mean_in_last_gemm_bit_identical(entry):
+    """fc7 = RCNN_top(pool5).mean(3).mean(2) taken inside the last conv3's GEMM function
+    (ResNetTop(..., mean=True) -> LinearActFunction mean_hw) against head_mean over the
+    channels-last output: fc7, the input gradient and every weight gradient bit for bit."""
+    from tlod.detector.resnet import ResNetTop, HeadEntry, _make_layer, head_mean
+    g = torch.Generator().manual_seed(11)
+    layer = _make_layer(1024, 512, 3, stride=2)
+    for m in layer.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            _rand_bn(m, g)
+            for p in m.parameters():
+                p.requires_grad = False
+        elif isinstance(m, torch.nn.Conv2d):
+            with torch.no_grad():
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * (2.0 / m.weight[0].numel()) ** 0.5)
+    top = ResNetTop(layer).to(dev)
+    R, H = 37, 4 if entry else 7
+    x = torch.randn(R, H, H, 1024, generator=g).to(dev)
+    gy = torch.randn(R, 2048, generator=g).to(dev)
+
+    def run(fused):
+        for p in top.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        inp = HeadEntry(xi) if entry else xi.permute(0, 3, 1, 2)
+        f = top(inp, mean=True) if fused else head_mean(top(inp))
+        assert f.shape == (R, 2048)
+        (f * gy).sum().backward()
+        return [f.detach(), xi.grad] + [p.grad for p in top.parameters() if p.requires_grad]
+    a, b = run(True), run(False)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), i
+
+
 LOSSES = ["rpn_loss_cls", "rpn_loss_box", "RCNN_loss_cls", "RCNN_loss_bbox", "DA_img_loss_cls",
           "DA_ins_loss_cls", "tgt_DA_img_loss_cls", "tgt_DA_ins_loss_cls", "DA_cst_loss",
           "tgt_DA_cst_loss"]

@@ -29,7 +29,6 @@ from ..roi_pool import _RoIPooling
 from ..rpn.proposal import proposals_on_side_streams
 from ..rpn.proposal_target import _ProposalTargetLayer
 from ..rpn.rpn_head import _RPN
-from ..detector import resnet as _resnet_mod
 
 
 class GRLayer(torch.autograd.Function):
@@ -347,4 +346,4 @@ class resnet(_fasterRCNN):
 
     def _head_to_tail(self, pool5):
         # RCNN_top(pool5).mean(3).mean(2) (resnet.py:286-288); the head runs channels-last
-        return _resnet_mod.head_mean(self.RCNN_top(pool5))
+        return self.RCNN_top(pool5, mean=True)

@@ -24,7 +24,6 @@ from ..rpn.proposal_target import _ProposalTargetLayer
 from ..rpn.rpn_head import _RPN
 from .losses import fused_losses, rcnn_losses, smooth_l1_loss, weighted_loss_sum
 from .vgg16 import vgg16_base, vgg16_top
-from . import resnet as _resnet_mod
 
 
 class _fasterRCNN(nn.Module):
@@ -174,4 +173,4 @@ class resnet(_fasterRCNN):
         return resnet_pool(self, feat, rois, _fasterRCNN._pool)
 
     def _head_to_tail(self, pool5):
-        return _resnet_mod.head_mean(self.RCNN_top(pool5))
+        return self.RCNN_top(pool5, mean=True)

@@ -180,11 +180,13 @@ class Bottleneck(nn.Module):
 
     # ---------------------------------------------------------------- RoI head path
     @staticmethod
-    def _gemm_bn(xm, conv, bn, relu, residual=None, relu_in=False, link=None, role=0):
+    def _gemm_bn(xm, conv, bn, relu, residual=None, relu_in=False, link=None, role=0,
+                 mean_hw=None):
         """xm: (P, Cin) channels-last rows; conv as a GEMM + folded BN (+res) (+ReLU).
         relu_in: xm is a ReLU output (its input gradient is masked in the GEMM epilogue);
         link / role: the identity shortcut's gradient handed from conv3 (role 3) to conv1
-        (role 1) — see LinearActFunction."""
+        (role 1) — see LinearActFunction.  mean_hw = (R, H, W): return the head's spatial
+        mean (R, Cout) instead of the rows (split-bf16 path only; the caller checks)."""
         scale, shift = fold_bn(bn)
         w = conv.weight
         wm = w.view(w.shape[0], -1) if w.shape[2] == 1 else w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
@@ -203,12 +205,14 @@ class Bottleneck(nn.Module):
         with torch.no_grad():
             wf = (wm * scale[:, None]).contiguous()
         return LinearActFunction.apply(xm.contiguous(), wf, shift, residual, relu, m, relu_in,
-                                       link, role, w, scale)
+                                       link, role, w, scale, mean_hw)
 
-    def forward_nhwc(self, x, subsampled=False, shape=None, relu_in=False):
+    def forward_nhwc(self, x, subsampled=False, shape=None, relu_in=False, mean=False):
         """The layer4 RoI head, channels-last.  x: (R, H, W, C), or (R*H*W, C) rows with
         shape = (R, H, W) (a previous block's output, relu_in = True); returns (rows, shape).
-        subsampled: x is already the stride-2 subsample (the head entry, HeadEntry)."""
+        subsampled: x is already the stride-2 subsample (the head entry, HeadEntry).
+        mean (the head's last block): when the fused path runs, returns (the spatial mean
+        (R, C), None) — fc7 of _head_to_tail — taken inside conv3's GEMM function."""
         if shape is None:
             if self.stride == 2 and not subsampled:
                 x = x[:, ::2, ::2, :]
@@ -230,8 +234,11 @@ class Bottleneck(nn.Module):
         self._tap("r2", out.view(R, H, W, P), nhwc=True)
         res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False)
                if self.downsample is not None else xm)
+        fuse_mean = mean and fused and self.act_tap is None
         out = self._gemm_bn(out, self.conv3, self.bn3, relu=True, residual=res, relu_in=fused,
-                            link=link, role=3)
+                            link=link, role=3, mean_hw=(R, H, W) if fuse_mean else None)
+        if fuse_mean:
+            return out, None
         self._tap("r3", out.view(R, H, W, -1), nhwc=True)
         return out, (R, H, W)
 
@@ -290,16 +297,23 @@ class ResNetTop(nn.Sequential):
     """RCNN_top = Sequential(layer4); forward(pool5 NCHW, or the HeadEntry) -> channels-last
     features."""
 
-    def forward(self, pool5):
+    def forward(self, pool5, mean=False):
+        """mean: return fc7 = out.mean(3).mean(2) of the NCHW reference (resnet.py:286-288),
+        (R, C), taken in the last GEMM function when it can (LinearActFunction mean_hw)."""
         if isinstance(pool5, HeadEntry):
             x, sub = pool5.x, True
         else:
             x, sub = pool5.permute(0, 2, 3, 1), False
         shape = None
-        for i, block in enumerate(self[0]):
-            x, shape = block.forward_nhwc(x, subsampled=sub and i == 0,
-                                          shape=shape, relu_in=shape is not None)
-        return x.view(*shape, x.shape[-1])
+        blocks = list(self[0])
+        for i, block in enumerate(blocks):
+            x, shape = block.forward_nhwc(x, subsampled=sub and i == 0, shape=shape,
+                                          relu_in=shape is not None,
+                                          mean=mean and i == len(blocks) - 1)
+            if shape is None:  # the mean was taken by the last block
+                return x
+        y = x.view(*shape, x.shape[-1])
+        return head_mean(y) if mean else y
 
 
 class HeadMeanFunction(torch.autograd.Function):

@@ -139,16 +139,23 @@ class LinearActFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, relu, math, relu_in=False, link=None, role=0,
-                wsrc=None, wscale=None):
+                wsrc=None, wscale=None, mean_hw=None):
         R, I = x.shape
         O = weight.shape[0]
         y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math, residual=residual, relu=relu)
+        ctx.mean_hw = mean_hw
         ctx.math, ctx.relu = math, relu
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
         ctx.params = (weight, bias)
         ctx.relu_in, ctx.link, ctx.role = bool(relu_in), link, role
         ctx.wsrc, ctx.wscale = wsrc, wscale
         ctx.save_for_backward(x, weight, y if relu else None)
+        if mean_hw is not None:
+            # the ResNet head's fc7 = y.view(R, H, W, O).mean(2).mean(1) (resnet.py:286-288)
+            # taken here, so the backward builds its gradient straight from the (R, O) mean
+            # gradient (no (R*H*W, O) broadcast materialised by a view's backward)
+            Rr, H, W = mean_hw
+            return y.view(Rr, H, W, O).mean(2).mean(1)
         return y
 
     @staticmethod
@@ -156,8 +163,16 @@ class LinearActFunction(torch.autograd.Function):
         x, weight, y = ctx.saved_tensors
         R, I = x.shape
         O = weight.shape[0]
-        if ctx.relu and getattr(dy, "_tlod_relu_masked", None) == (y.data_ptr(), dy.data_ptr(),
-                                                                   dy._version):
+        if ctx.mean_hw is not None:  # dy: (Rr, O), the two means' backward is (dy / H) / W
+            Rr, H, W = ctx.mean_hw
+            gb = ((dy / H) / W)[:, None, :].expand(Rr, H * W, O)
+            if ctx.relu:
+                g = torch.where(y.view(Rr, H * W, O) > 0, gb,
+                                torch.zeros((), dtype=dy.dtype, device=dy.device)).view(R, O)
+            else:
+                g = gb.reshape(R, O)
+        elif ctx.relu and getattr(dy, "_tlod_relu_masked", None) == (y.data_ptr(), dy.data_ptr(),
+                                                                     dy._version):
             g = dy  # masked by the consumer's input-gradient epilogue
             STATS["relu_bwd_skipped"] += 1
         elif ctx.relu:  # (one pass: dy may be a broadcast view, e.g. the head's mean backward)
@@ -194,7 +209,7 @@ class LinearActFunction(torch.autograd.Function):
         dres = g if ctx.has_res and ctx.needs_input_grad[3] else None
         if dres is not None and ctx.role == 3 and ctx.link is not None:
             ctx.link.g, dres = dres, None  # to conv1's backward
-        return dx, dw, db, dres, None, None, None, None, None, dsrc, None
+        return dx, dw, db, dres, None, None, None, None, None, dsrc, None, None
 
 
 class Linear(nn.Linear):
