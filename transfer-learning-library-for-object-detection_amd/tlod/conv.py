@@ -505,10 +505,13 @@ class ShortcutLink:
     first) to its conv1's backward, whose input is the same tensor: conv1's dgrad adds it in
     the epilogue before the previous block's ReLU mask (tlod_conv1x1_gemm_bs_ex_f32), instead
     of autograd summing the two gradients and the previous block running a ReLU-backward pass
-    over the sum."""
+    over the sum.  The RoI head's downsample blocks use it the same way for the downsample
+    conv's input gradient (LinearActFunction role 4); `consumed` marks that conv1's backward
+    has run, so a role-4 backward scheduled after it keeps its gradient for autograd."""
 
     def __init__(self):
         self.g = None
+        self.consumed = False
 
 
 class ConvBNFunction(torch.autograd.Function):

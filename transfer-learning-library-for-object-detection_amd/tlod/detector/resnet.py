@@ -222,9 +222,11 @@ class Bottleneck(nn.Module):
             assert self.stride == 1 or subsampled
             (R, H, W), xm = shape, x
         fused = linear_math() != "f32" and os.environ.get("TLOD_HEAD_FUSE", "1") != "0"
-        # identity shortcut: conv1's input gradient takes the shortcut's gradient (HeadLink)
-        link = (ShortcutLink() if fused and self.downsample is None and self.stride == 1
-                else None)
+        # identity shortcut: conv1's input gradient takes the shortcut's gradient (conv3's
+        # residual gradient, role 3); downsample shortcut: it takes the downsample conv's
+        # input gradient (role 4) — either way one GEMM epilogue instead of autograd's sum
+        identity = self.downsample is None and self.stride == 1
+        link = ShortcutLink() if fused and (identity or self.downsample is not None) else None
         out = self._gemm_bn(xm, self.conv1, self.bn1, relu=True, relu_in=fused and relu_in,
                             link=link, role=1)
         P = out.shape[1]
@@ -232,11 +234,13 @@ class Bottleneck(nn.Module):
         taps = im2col3x3_nhwc(out, (R, H, W), relu_in=fused)
         out = self._gemm_bn(taps, self.conv2, self.bn2, relu=True)
         self._tap("r2", out.view(R, H, W, P), nhwc=True)
-        res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False)
+        res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False,
+                             link=link, role=4)
                if self.downsample is not None else xm)
         fuse_mean = mean and fused and self.act_tap is None
         out = self._gemm_bn(out, self.conv3, self.bn3, relu=True, residual=res, relu_in=fused,
-                            link=link, role=3, mean_hw=(R, H, W) if fuse_mean else None)
+                            link=link if identity else None, role=3 if identity else 0,
+                            mean_hw=(R, H, W) if fuse_mean else None)
         if fuse_mean:
             return out, None
         self._tap("r3", out.view(R, H, W, -1), nhwc=True)

@@ -130,7 +130,8 @@ class LinearActFunction(torch.autograd.Function):
     (gemm_mask) and tagged, so that layer's backward skips its own mask pass (a gradient that
     arrives tagged for this y is already g).  link (a tlod.conv.ShortcutLink) / role: an
     identity bottleneck's conv3 (role 3) hands its residual gradient g to conv1 (role 1),
-    whose input gradient adds it in the same epilogue — no autograd sum of the two.
+    whose input gradient adds it in the same epilogue — no autograd sum of the two; a
+    downsample block's shortcut conv (role 4) hands conv1 its input gradient the same way.
     wsrc / wscale (a conv weight (O, C, kh, kw) and a per-output scale): `weight` is the GEMM
     form of wsrc * wscale (rows (kh, kw, c) for 3x3), computed by the caller without autograd;
     the backward writes d wsrc = (dy^T x in the GEMM form) * wscale, re-laid out, straight
@@ -182,6 +183,7 @@ class LinearActFunction(torch.autograd.Function):
         res = None
         if ctx.role == 1 and ctx.link is not None:
             res, ctx.link.g = ctx.link.g, None
+            ctx.link.consumed = True  # a role-4 backward running later returns its own dx
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             if ctx.relu_in:
@@ -190,6 +192,9 @@ class LinearActFunction(torch.autograd.Function):
                 dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math, residual=res)
         if ctx.needs_input_grad[1]:
             dw = gemm(g, x, O, I, R, 0, 0, None, ctx.math, out=grad_out(ctx.params[0]))
+        if (dx is not None and ctx.role == 4 and ctx.link is not None
+                and not getattr(ctx.link, "consumed", False)):
+            ctx.link.g, dx = dx, None  # to conv1's input-gradient GEMM (role 1)
         dsrc = None
         if ctx.wsrc is not None and ctx.needs_input_grad[9]:
             w = ctx.wsrc
