@@ -52,8 +52,10 @@ __global__ void __launch_bounds__(256) conv3x3_direct_kernel(const float* __rest
       const f2 xk = {in[k], in[k]};
       acc = __builtin_elementwise_fma(xk, wk, acc);
     }
-    yp[(size_t)co * HW] = relu ? fmaxf(acc.x, 0.f) : acc.x;
-    yp[(size_t)(co + 1) * HW] = relu ? fmaxf(acc.y, 0.f) : acc.y;
+    // streaming stores: the 64-channel output (368 MB for two 600x1200 images) is read back
+    // only by conv1_2, long after it has left the caches
+    __builtin_nontemporal_store(relu ? fmaxf(acc.x, 0.f) : acc.x, yp + (size_t)co * HW);
+    __builtin_nontemporal_store(relu ? fmaxf(acc.y, 0.f) : acc.y, yp + (size_t)(co + 1) * HW);
   }
   if (co < Cout) {
     const float* wc = w + co * CIN * 9;
