@@ -57,6 +57,38 @@ def test_params_without_grad_are_skipped():
     assert all(p.grad is None for p in unused.parameters())
 
 
+def test_fast_table_key_matches_slow_path(monkeypatch):
+    """The descriptor table's fast key (every gradient arrived in its arena slot since the
+    last zero_grad: no per-parameter host work) against the optimizer without an arena
+    (per-pointer key every step), over steps with all gradients, a step where one module
+    gets none, and a step with no zero_grad in between: parameters bit-identical."""
+    from tlod.optim import FusedSGDClip
+
+    def build(arena):
+        monkeypatch.setenv("TLOD_GRAD_ARENA", "1" if arena else "0")
+        torch.manual_seed(0)
+        m1, m2 = torch.nn.Linear(64, 32).cuda(), torch.nn.Linear(32, 16).cuda()
+        opt = FusedSGDClip([{"params": list(m1.parameters()) + list(m2.parameters()),
+                             "lr": 0.05, "weight_decay": 5e-4}], clip_norm=1.0)
+        return m1, m2, opt
+    runs = []
+    for arena in (True, False):
+        m1, m2, opt = build(arena)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        for step, (both, zero) in enumerate([(1, 1), (1, 1), (0, 1), (1, 1), (1, 0), (1, 1)]):
+            if zero:
+                opt.zero_grad()
+            x = torch.randn(8, 64, device="cuda", generator=g)
+            h = m1(x)
+            (m2(h).square().mean() if both else h.square().mean()).backward()
+            opt.step()
+        if arena:
+            assert opt.table_builds <= 3  # all-gradient steps share one table
+        runs.append([p.detach().clone() for p in list(m1.parameters()) + list(m2.parameters())])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("clip", [0.0, 10.0])
 def test_fused_pack_update(clip, monkeypatch):
     """tlod_sgd_clip_pack_f32: the 3x3 weights a FusedSGDClip owns are updated by tiles that

@@ -43,6 +43,8 @@ class GradArena:
         self.index = {p: i for i, p in enumerate(params)}
         self.gen = 0
         self._claimed = {}
+        self._seen = {}
+        self.n_seen = 0  # parameters whose gradient arrived (in its slot) this generation
         self.listeners = []
         self.tail_len = 0
         self.active = None  # per-parameter gradient-producer counts (tail view), DP only
@@ -93,6 +95,7 @@ class GradArena:
 
     def zero_grad(self):
         self.gen += 1
+        self.n_seen = 0
         for p in self.params:
             p.grad = None
 
@@ -103,6 +106,9 @@ class GradArena:
             v = self.view(p)
             v.copy_(g)
             p.grad = v
+        if self._seen.get(p) != self.gen:
+            self._seen[p] = self.gen
+            self.n_seen += 1
         for cb in self.listeners:
             cb(p)
 
