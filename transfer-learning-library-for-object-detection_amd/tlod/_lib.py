@@ -12,6 +12,25 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libtlod.so")
+# os.environ's own bytes mapping: the hot-path switches (math mode, fusion toggles) are read
+# per conv / GEMM call, and os.environ.get's per-call key encode + value decode cost ~1 us
+# each (~1.3k reads per ATF-R101 step; the A/B was step-neutral, profiles/r05/host_env_ab.txt).
+# A plain dict lookup on the same mapping sees exported and monkeypatched values alike.
+_ENV_DATA = getattr(os.environ, "_data", None)
+_ENV_KEYS = {}
+
+
+def env(name, default=None):
+    """os.environ.get(name, default), without the per-call encode / decode."""
+    if _ENV_DATA is None:
+        return os.environ.get(name, default)
+    k = _ENV_KEYS.get(name)
+    if k is None:
+        k = _ENV_KEYS[name] = os.fsencode(name)
+    v = _ENV_DATA.get(k)
+    return default if v is None else os.fsdecode(v)
+
+
 if os.environ.get("TLOD_LIB"):  # tuning builds (tools/build_variants.sh); same ABI
     LIB_PATH = os.environ["TLOD_LIB"]
 

@@ -68,7 +68,7 @@ def conv_math():
     input and output channels (the ResNet bottlenecks, DA heads) run their forward / input
     gradient on the split-bf16 conv GEMM too (_gemm1x1), narrower ones (RPN heads) on the
     f32-input MFMA."""
-    m = os.environ.get("TLOD_CONV_MATH", "bf16x6")
+    m = _lib.env("TLOD_CONV_MATH", "bf16x6")
     if m not in MATHS:
         raise ValueError(f"TLOD_CONV_MATH={m!r}: expected one of {MATHS}")
     return m
@@ -92,7 +92,7 @@ def _gemm_conv(KS, math, out_channels):
     patch-staged kernel (tlod_conv_fwd_bs_f32).  Opt-in (TLOD_CONV_GEMM=1): measured equal
     to the patch-staged kernel in the DAF step (conv3_3 fwd 0.558 vs 0.553 ms)."""
     return (_bs(KS, math) and out_channels >= 256
-            and os.environ.get("TLOD_CONV_GEMM", "0") != "0")
+            and _lib.env("TLOD_CONV_GEMM", "0") != "0")
 
 
 def _gemm1x1(KS, math, cin, cout):
@@ -104,8 +104,8 @@ def _gemm1x1(KS, math, cin, cout):
     mostly padding still beats the f32-input MFMA kernel's 6.6 TF); TLOD_CONV1X1_BS=0 keeps
     them on the f32-input MFMA kernel."""
     return (KS == 1 and math != "f32" and max(cin, cout) >= 64
-            and min(cin, cout) >= int(os.environ.get("TLOD_CONV1X1_MIN", "16"))
-            and os.environ.get("TLOD_CONV1X1_BS", "1") != "0")
+            and min(cin, cout) >= int(_lib.env("TLOD_CONV1X1_MIN", "16"))
+            and _lib.env("TLOD_CONV1X1_BS", "1") != "0")
 
 
 def _conv_gemm(x, w, w_layout, bias, relu, scale, residual, Cout, math, kind, KS=3, mask=None,
@@ -374,7 +374,7 @@ def wgrad_math():
     """Arithmetic of the 3x3 weight gradients (env TLOD_WGRAD_MATH, default: the
     TLOD_CONV_MATH choice): "bf16x6" / "bf16x3" run tlod_conv_wgrad_bs_f32 (split-bf16,
     same slab reduction), "f32" the f32-input MFMA kernel."""
-    m = os.environ.get("TLOD_WGRAD_MATH") or conv_math()
+    m = _lib.env("TLOD_WGRAD_MATH") or conv_math()
     if m not in MATHS:
         raise ValueError(f"TLOD_WGRAD_MATH={m!r}: expected one of {MATHS}")
     return m

@@ -1,14 +1,14 @@
 """Detector losses (lib/model/utils/net_utils.py:72-86, lib/model/rpn/rpn.py:89-108)."""
-import os
-
 import torch
 import torch.nn.functional as F
+
+from .. import _lib
 
 
 def fused_losses():
     """TLOD_FUSED_LOSSES (default 1): the one-launch libtlod losses below; 0 = the torch
     compositions (A/B comparison and tests)."""
-    return os.environ.get("TLOD_FUSED_LOSSES", "1") != "0"
+    return _lib.env("TLOD_FUSED_LOSSES", "1") != "0"
 
 
 def smooth_l1_loss(bbox_pred, bbox_targets, inside_w, outside_w, sigma=1.0, dim=(1,)):

@@ -18,7 +18,6 @@ in eval mode (:249-284).  Execution:
     would fill 16 of the 256 pixel slots of a conv tile.
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -221,7 +220,7 @@ class Bottleneck(nn.Module):
         else:
             assert self.stride == 1 or subsampled
             (R, H, W), xm = shape, x
-        fused = linear_math() != "f32" and os.environ.get("TLOD_HEAD_FUSE", "1") != "0"
+        fused = linear_math() != "f32" and _lib.env("TLOD_HEAD_FUSE", "1") != "0"
         # identity shortcut: conv1's input gradient takes the shortcut's gradient (conv3's
         # residual gradient, role 3); downsample shortcut: it takes the downsample conv's
         # input gradient (role 4) — either way one GEMM epilogue instead of autograd's sum
@@ -290,7 +289,7 @@ def resnet_pool(model, feat, rois, base_pool):
     ra = model.RCNN_roi_align
     first = model.RCNN_top[0][0]
     if (cfg.POOLING_MODE == "align" and ra.aligned_height <= 7 and ra.aligned_width <= 7
-            and first.stride == 2 and os.environ.get("TLOD_ROI_HEAD_ENTRY", "1") != "0"):
+            and first.stride == 2 and _lib.env("TLOD_ROI_HEAD_ENTRY", "1") != "0"):
         from ..roi_align import roi_align_avg_s2_nhwc
         return HeadEntry(roi_align_avg_s2_nhwc(feat, rois, ra.aligned_height, ra.aligned_width,
                                                ra.spatial_scale))

@@ -9,7 +9,6 @@ accumulation: f32-level error, tests/test_linear_gpu.py); the bias gradient is a
 sum.  Layers narrower than one 256-wide tile (the 9-way class / 36-way box heads, the
 1-way DA classifier) stay on nn.Linear, where a 256x256 tile would be mostly padding.
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -23,7 +22,7 @@ MATHS = ("bf16x6", "bf16x3")
 def linear_math():
     """TLOD_LINEAR_MATH: "bf16x6" (default, f32-level error), "bf16x3" (~5e-6), or "f32"
     (nn.Linear's GEMM library path, for A/B comparison)."""
-    m = os.environ.get("TLOD_LINEAR_MATH", "bf16x6")
+    m = _lib.env("TLOD_LINEAR_MATH", "bf16x6")
     if m not in MATHS + ("f32",):
         raise ValueError(f"TLOD_LINEAR_MATH={m!r}")
     return m
@@ -230,7 +229,7 @@ class Linear(nn.Linear):
 def fused_act():
     """TLOD_FUSED_ACT (default 1): ReLU + dropout after the head's Linear layers as one
     libtlod pass each way (tlod_relu_dropout_f32); 0 = nn.ReLU + nn.Dropout."""
-    return os.environ.get("TLOD_FUSED_ACT", "1") != "0"
+    return _lib.env("TLOD_FUSED_ACT", "1") != "0"
 
 
 class ReluDropoutFunction(torch.autograd.Function):
