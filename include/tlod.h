@@ -474,7 +474,10 @@ int tlod_col2im3x3_nhwc_mask_f32(const float* col, int R, int H, int W, int C, c
  * active: NULL, or a device float; a chunk whose *active == 0 is left untouched (data
  * parallel: the number of ranks that produced the gradient, all-reduced with it — a
  * parameter no rank used is skipped like a None .grad in torch.optim.SGD; its gradient
- * slot is zero, so it adds nothing to the norm). */
+ * slot is zero, so it adds nothing to the norm).
+ * count < 0: the chunk's -count elements only enter the gradient norm (their parameter is
+ * updated by tlod_sgd_clip_pack_f32's tiles), so a table lists every parameter in one order
+ * whether or not packs are kept. */
 typedef struct tlod_sgd_chunk {
   float* param;
   const float* grad;
@@ -491,8 +494,9 @@ int tlod_sgd_clip_f32(const tlod_sgd_chunk* chunks, int n_chunks, float grad_sca
 
 /* The same step with the split-bf16 weight packs of 3x3 conv weights written by the update
  * itself (no per-weight tlod_conv_pack_bs launches before the next forward / backward).
- * chunks[0, n_update) are updated as above; chunks[n_update, n_chunks) only enter the
- * gradient norm: their parameters are the 3x3 weights the tiles update.  A tile is 32 output
+ * chunks[0, n_update) are updated as above (except norm-only rows, count < 0);
+ * chunks[n_update, n_chunks) only enter the gradient norm: their parameters are the 3x3
+ * weights the tiles update.  A tile is 32 output
  * x 32 input channels x 9 taps of one (cout, cin, 3, 3) weight (o0, i0: its first output /
  * input channel, multiples of 32); it applies the SGD update to its elements and stores the
  * new weights into each non-NULL pack — pack_fwd: the tlod_conv_pack_bs(dgrad = 0) layout,

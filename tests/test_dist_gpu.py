@@ -42,13 +42,19 @@ def _batch(rank, step, dev):
     return tuple(b)
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, reserve=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
+    if reserve is not None:  # the nccl-only CU reserve, forced under gloo
+        os.environ["TLOD_DIST_CU_RESERVE"] = str(reserve)
     sys.path.insert(0, PKG)
     import torch.distributed as dist
+    import tlod.dist as td
     from tlod.detector.train import build_model, make_optimizer, train_step
     from tlod.dist import GradBucketReducer
+    calls = []
+    real_set = td._set_cu_reserve
+    td._set_cu_reserve = lambda n: (calls.append(int(n)), real_set(n))[1]
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -68,16 +74,25 @@ def _worker(rank, world, port, outdir):
         torch.cuda.synchronize()
         rec[f"g{step}"] = {k: v.cpu() for k, v in local.items()}
         rec[f"w{step + 1}"] = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    rec["reserve_calls"] = torch.tensor(calls, dtype=torch.int64)
     torch.save(rec, os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_daf_vgg16_data_parallel_two_ranks(tmp_path):
+@pytest.mark.parametrize("reserve", [None, 32])
+def test_daf_vgg16_data_parallel_two_ranks(tmp_path, reserve):
+    """reserve=32: TLOD_DIST_CU_RESERVE forced under gloo, so the reducer's reserve toggle
+    (on at the first bucket's launch, off after finish(): tlod.dist) runs every backward of
+    both steps, and each rank's conv / GEMM launches after fc6's bucket execute the plans for
+    224 CUs that the 8-GPU RCCL run uses; the device-tensor broadcast of the first step's
+    bucket order runs too (the arena lives on cuda:0)."""
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), reserve), nprocs=2, join=True)
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    want = [32, 0, 32, 0] if reserve else []
+    assert r0["reserve_calls"].tolist() == want and r1["reserve_calls"].tolist() == want
     for step in (1, 2):
         for k in r0[f"w{step}"]:
             assert torch.equal(r0[f"w{step}"][k], r1[f"w{step}"][k]), (step, k)

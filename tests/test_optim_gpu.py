@@ -94,8 +94,9 @@ def test_fused_pack_update(clip, monkeypatch):
     """tlod_sgd_clip_pack_f32: the 3x3 weights a FusedSGDClip owns are updated by tiles that
     also write their split-bf16 packs.  After every step the packs the convs will use (the
     cached ones: no re-pack, PACK_GEN unchanged) are bit-identical to packs made from the
-    updated weights, and the weights match the chunk-only update (TLOD_SGD_PACK=0) — bit for
-    bit without clipping (with it the norm's partials are summed in another order).  Ragged
+    updated weights, and the weights match the chunk-only update (TLOD_SGD_PACK=0) bit for
+    bit, with and without clipping (the norm's chunk rows are in parameter order either way,
+    round-5 advisor).  Ragged
     channel counts (tiles past the last channel), a BN-scaled input-gradient pack, Cin = 3."""
     from tlod import conv
     from tlod.optim import FusedSGDClip
@@ -132,10 +133,7 @@ def test_fused_pack_update(clip, monkeypatch):
             sum((p * r).sum() for p, r in zip(ps, rs)).backward()
             opt.step()
         for a, b in zip(pa, pb):
-            if clip == 0:
-                assert torch.equal(a.detach(), b.detach())
-            else:
-                torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-7)
+            assert torch.equal(a.detach(), b.detach())
         now = packs()
         assert conv.PACK_GEN[0] == gen and all(x is y for x, y in zip(now, first))
         fresh = []
@@ -147,3 +145,31 @@ def test_fused_pack_update(clip, monkeypatch):
     # a trainable weight no fused optimizer owns is packed afresh on every use
     w = torch.nn.Parameter(torch.randn(8, 8, 3, 3, device="cuda"))
     assert conv.pack_bs(w, False) is not conv.pack_bs(w, False)
+
+
+@pytest.mark.parametrize("order", ["plain_after", "plain_before"])
+def test_plain_update_never_leaves_stale_packs(order, monkeypatch):
+    """Round-5 advisor: a weight owned by a pack-writing FusedSGDClip that another optimizer
+    updates with the plain kernel (TLOD_SGD_PACK=0; its writes bump no version).  Built after
+    the owner, the plain optimizer takes the ownership back; built before, it drops the
+    owner's cached packs after each of its steps.  Either way the pack the next conv gets is
+    bit-identical to a fresh pack of the current weight."""
+    from tlod import conv
+    from tlod.optim import FusedSGDClip
+    torch.manual_seed(5)
+    w = torch.nn.Parameter(torch.randn(48, 40, 3, 3, device="cuda") * 0.05)
+    mk = lambda packs: (monkeypatch.setenv("TLOD_SGD_PACK", "1" if packs else "0"),
+                        FusedSGDClip([{"params": [w], "lr": 0.01, "weight_decay": 5e-4}],
+                                     momentum=0.9, clip_norm=10.0))[1]
+    if order == "plain_after":
+        fused, plain = mk(True), mk(False)
+    else:
+        plain, fused = mk(False), mk(True)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for opt in (fused, plain, plain, fused, plain):
+        conv.pack_bs(w, False), conv.pack_bs(w, True)  # cache (or not) the current packs
+        opt.zero_grad()
+        (w * torch.randn(w.shape, device="cuda", generator=g)).sum().backward()
+        opt.step()
+        assert torch.equal(conv.pack_bs(w, False), conv._pack_bs(w, False))
+        assert torch.equal(conv.pack_bs(w, True), conv._pack_bs(w, True))

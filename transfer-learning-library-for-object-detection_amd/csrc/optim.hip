@@ -37,7 +37,8 @@ __device__ __forceinline__ bool vec4_ok(const void* a, const void* b, const void
 
 __global__ void __launch_bounds__(256) sgd_sumsq_kernel(const tlod_sgd_chunk* __restrict__ chunks,
                                                         float gs, float* __restrict__ partials) {
-  const tlod_sgd_chunk c = chunks[blockIdx.x];
+  tlod_sgd_chunk c = chunks[blockIdx.x];
+  c.count = c.count < 0 ? -c.count : c.count;  // (a norm-only row: see tlod_sgd_chunk)
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (vec4_ok(c.grad, c.grad, c.grad, c.count)) {
     typedef float v4 __attribute__((ext_vector_type(4)));
@@ -92,6 +93,7 @@ __global__ void __launch_bounds__(256) sgd_update_kernel(const tlod_sgd_chunk* _
                                                          const float* __restrict__ norm_scale,
                                                          float gs, float momentum) {
   const tlod_sgd_chunk c = chunks[blockIdx.x];
+  if (c.count < 0) return;  // norm-only row: a pack tile updates these elements
   if (c.active != nullptr && *c.active == 0.f) return;  // no rank produced this gradient
   const float scale = norm_scale[1];
   if (vec4_ok(c.grad, c.param, c.momentum_buf, c.count)) {

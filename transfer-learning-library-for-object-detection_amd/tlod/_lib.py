@@ -18,6 +18,13 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libtlod.so")
 # A plain dict lookup on the same mapping sees exported and monkeypatched values alike.
 _ENV_DATA = getattr(os.environ, "_data", None)
 _ENV_KEYS = {}
+# CPython-private layout (POSIX: a dict of fsencoded bytes keys and values); anything else —
+# Windows' upper-cased str keys, a future _Environ — takes os.environ.get (round-5 advisor)
+if not (os.name == "posix" and type(_ENV_DATA) is dict
+        and all(isinstance(k, bytes) and isinstance(v, bytes) for k, v in _ENV_DATA.items())
+        and os.environ.get("PATH") == (os.fsdecode(_ENV_DATA[b"PATH"]) if b"PATH" in _ENV_DATA
+                                       else None)):
+    _ENV_DATA = None
 
 
 def env(name, default=None):

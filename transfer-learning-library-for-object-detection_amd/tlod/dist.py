@@ -91,6 +91,7 @@ class GradBucketReducer:
         backend = dist.get_backend(group)
         self.cu_reserve = int(os.environ.get("TLOD_DIST_CU_RESERVE",
                                              "32" if backend == "nccl" else "0"))
+        self._reserve_on = False
         self._build_buckets()
         arena.listeners.append(self._on_grad)
 
@@ -119,6 +120,9 @@ class GradBucketReducer:
         self._reset()
 
     def _reset(self):
+        # a step abandoned before finish() (an exception in backward, zero_grad) must not
+        # leave every later launch planned for fewer CUs (round-5 advisor)
+        self._clear_reserve()
         for b in self.buckets:
             b["ready"], b["work"] = 0, None
         self.next = 0  # first bucket of the static list not yet launched
@@ -140,6 +144,7 @@ class GradBucketReducer:
                 return
             if self.next == 0 and self.cu_reserve:
                 _set_cu_reserve(self.cu_reserve)
+                self._reserve_on = True
             b["work"] = dist.all_reduce(self._flat(b), op=dist.ReduceOp.SUM, group=self.group,
                                         async_op=True)
             self.next += 1
@@ -189,8 +194,7 @@ class GradBucketReducer:
         self._launch_ready_prefix()
         for b in self.buckets:
             b["work"].wait()
-        if self.cu_reserve:
-            _set_cu_reserve(0)
+        self._clear_reserve()
         for p in unmarked:
             p.grad = a.view(p)
         seen = self.seen
@@ -205,13 +209,20 @@ class GradBucketReducer:
         self._reset()
         return seen
 
+    def _clear_reserve(self):
+        if getattr(self, "_reserve_on", False):
+            _set_cu_reserve(0)
+            self._reserve_on = False
+
     def _relayout(self, seen):
         """Adopt rank 0's gradient-ready order of the first step (broadcast, so every rank
         builds the same bucket list)."""
         self.relayout_pending = False
         n = len(self.arena.params)
         order = seen + [i for i in range(n) if i not in set(seen)]
-        dev = self.arena.flat.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        # the arena's device (RCCL; gloo broadcasts device tensors through the host), a CPU
+        # tensor for a CPU arena
+        dev = self.arena.flat.device
         t = torch.tensor(order, dtype=torch.int64, device=dev)
         dist.broadcast(t, dist.get_global_rank(self.group, 0) if self.group else 0,
                        group=self.group)

@@ -42,6 +42,7 @@ class GradArena:
         self.params = params
         self.index = {p: i for i, p in enumerate(params)}
         self.gen = 0
+        self.layout_gen = 0  # bumped by every layout(): keys tables built for a slot layout
         self._claimed = {}
         self._seen = {}
         self.n_seen = 0  # parameters whose gradient arrived (in its slot) this generation
@@ -67,6 +68,7 @@ class GradArena:
                            device=self.params[0].device)
         old, old_active = getattr(self, "flat", None), getattr(self, "active", None)
         self.order, self.offset, self.flat = order, offs, flat
+        self.layout_gen = getattr(self, "layout_gen", 0) + 1
         self.active = self.flat.narrow(0, off, len(self.params)) if self.tail_len else None
         if old_active is not None and self.active is not None:
             self.active.copy_(old_active)

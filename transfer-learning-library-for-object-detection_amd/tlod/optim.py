@@ -11,7 +11,12 @@ once per (arena layout, set of parameters with a gradient, learning rates).
 kernels' operand layouts, tlod_sgd_clip_pack_f32): the optimizer marks them as owned
 (`_tlod_pack_owner`), tlod.conv.pack_bs then caches their packs, and the next forward and
 backward use the packs this step wrote instead of re-packing every weight.  TLOD_SGD_PACK=0
-turns that off (every trainable 3x3 weight re-packed per use, as before).
+turns that off (every trainable 3x3 weight re-packed per use, as before; such an optimizer
+also takes back the ownership an earlier one claimed, and drops the cached packs of weights a
+later one claimed after each of its plain updates, so no pack outlives its weight).  Weight
+writes outside these optimizers that bypass the version counter (``p.data.*_()``, a direct
+tlod_sgd_clip_f32 call) must call tlod.conv.weights_updated(), as the data-parallel broadcast
+does.
 """
 import os
 
@@ -66,10 +71,16 @@ class FusedSGDClip:
         for p in self.params:
             _lib.require_cuda(p)
         self.fused_packs = os.environ.get("TLOD_SGD_PACK", "1") != "0"
-        if self.fused_packs:
-            for p in self.params:
-                if p.dim() == 4 and tuple(p.shape[2:]) == (3, 3):
+        for p in self.params:
+            if p.dim() == 4 and tuple(p.shape[2:]) == (3, 3):
+                if self.fused_packs:
                     p._tlod_pack_owner = True
+                elif getattr(p, "_tlod_pack_owner", False):
+                    # this optimizer's plain update would leave an earlier owner's cached
+                    # packs stale: the weight goes back to a repack per use (round-5 advisor)
+                    p._tlod_pack_owner = False
+                    p._tlod_packs = {}
+                    _conv.PACK_GEN[0] += 1
         dev = self.params[0].device
         self.bufs = [torch.zeros_like(p) for p in self.params]
         n_chunks = sum((p.numel() + CHUNK - 1) // CHUNK for p in self.params)
@@ -108,7 +119,7 @@ class FusedSGDClip:
         """Descriptor rows for every parameter that has a gradient (torch.optim.SGD skips
         the others entirely: no weight decay, no momentum update): (chunk table, tile table,
         rows updated by chunks, rows, tiles).  The 3x3 weights with packs get tiles; their
-        chunk rows come last and only enter the gradient norm."""
+        chunk rows (negative counts) only enter the gradient norm."""
         a = self.arena
         act = a.active if a is not None and a.active is not None else None
         tail = tuple(g["lr"] for g in self.param_groups) + \
@@ -119,14 +130,16 @@ class FusedSGDClip:
         # of Python per ResNet101 step, the GPU idling at the end of the backward)
         if fast and a is not None and a.n_seen == len(a.params) and \
                 all(arena_of(p) is a for p in self._fast_ok()):
-            key = ("all", id(a), a.flat.data_ptr()) + tail
+            # (the layout generation, not the buffer address: a relayout's new buffer may
+            # land where an earlier one was freed)
+            key = ("all", id(a), a.layout_gen) + tail
         else:
             key = tuple(0 if p.grad is None else p.grad.data_ptr() for p in self.params) + tail
         hit = self._tables.get(key)
         if hit is not None:
             return hit
         self.table_builds += 1
-        rows, norm_rows, tiles, keep = [], [], [], []
+        rows, tiles, keep = [], [], []
         idx = 0
         for g in self.param_groups:
             for p in g["params"]:
@@ -141,10 +154,13 @@ class FusedSGDClip:
                 ap = 0 if act is None else act.data_ptr() + 4 * a.index[p]
                 packs = _packs_of(p) if self.fused_packs and getattr(p, "_tlod_pack_owner",
                                                                      False) else None
-                dest = rows if packs is None else norm_rows
+                # every parameter's chunk rows in parameter order (the norm's summation order
+                # does not depend on TLOD_SGD_PACK); a negative count marks a norm-only row,
+                # whose elements the pack tiles update
+                sign = 1 if packs is None else -1
                 for off in range(0, n, CHUNK):
-                    dest.append((p.data_ptr() + 4 * off, gr.data_ptr() + 4 * off,
-                                 buf.data_ptr() + 4 * off, min(CHUNK, n - off), lr, wd, ap))
+                    rows.append((p.data_ptr() + 4 * off, gr.data_ptr() + 4 * off,
+                                 buf.data_ptr() + 4 * off, sign * min(CHUNK, n - off), lr, wd, ap))
                 if packs is None:
                     continue
                 keep.append(packs)  # the table holds their pointers
@@ -154,11 +170,11 @@ class FusedSGDClip:
                     for i0 in range(0, cin, TILE):
                         tiles.append((p.data_ptr(), gr.data_ptr(), buf.data_ptr(), ap, pf, pd,
                                       pds, sc, lr, wd, cout, cin, o0, i0, (0, 0)))
-        chunks = self._upload(np.array(rows + norm_rows, dtype=_DESC))
+        chunks = self._upload(np.array(rows, dtype=_DESC))
         tile_t = self._upload(np.array(tiles, dtype=_TILE))
         if len(self._tables) >= 8:
             self._tables.pop(next(iter(self._tables)))
-        hit = (chunks, tile_t, len(rows), len(rows) + len(norm_rows), len(tiles), keep)
+        hit = (chunks, tile_t, len(rows), len(rows), len(tiles), keep)
         self._tables[key] = hit
         return hit
 
@@ -185,4 +201,11 @@ class FusedSGDClip:
             _lib.ptr(chunks), n, n_update, _lib.ptr(tiles), n_tiles, float(grad_scale),
             self.momentum, self.clip_norm, _lib.ptr(self.partials), _lib.ptr(self.norm_scale),
             _lib.stream_of(self.partials)), "sgd_clip")
+        if not self.fused_packs:
+            # the plain update writes weights without a version bump: packs cached for a
+            # weight that a pack-writing optimizer claimed after this one was built are stale
+            for p in self.params:
+                if getattr(p, "_tlod_pack_owner", False) and getattr(p, "_tlod_packs", None):
+                    p._tlod_packs = {}
+                    _conv.PACK_GEN[0] += 1
         return self.norm_scale[0]
