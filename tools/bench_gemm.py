@@ -30,6 +30,11 @@ LAYERS = [("fc6", 25088, 4096), ("fc7", 4096, 4096)]
 if "--r101" in sys.argv:  # the DAF-R101 RoI head's layer4 GEMMs: 428 RoIs x 16 bins (4 x 4)
     R = 6848
     LAYERS = [("l4_conv1", 2048, 512), ("l4_conv2", 4608, 512), ("l4_conv3", 512, 2048)]
+if "--atf" in sys.argv:  # the ATF-R101 RoI head (config 5): 4512 RoIs x 16 bins through layer4
+    R = int(os.environ.get("ATF_ROWS", 4512 * 16))
+    LAYERS = [("l4b0_conv1", 1024, 512), ("l4_conv1", 2048, 512), ("l4_conv2", 4608, 512),
+              ("l4_conv3", 512, 2048), ("l4_ds", 1024, 2048)]
+NOTORCH = "--no-torch" in sys.argv
 for name, I, O in LAYERS:
     x = torch.randn(R, I, device="cuda")
     w = torch.randn(O, I, device="cuda") * 0.01
@@ -39,7 +44,8 @@ for name, I, O in LAYERS:
             ("fwd", lambda: gemm(x, w, R, O, I, 1, 1), lambda: x @ w.t()),
             ("dgrad", lambda: gemm(dy, w, R, I, O, 1, 0), lambda: dy @ w),
             ("wgrad", lambda: gemm(dy, x, O, I, R, 0, 0), lambda: dy.t() @ x)):
-        ms, tms = timeit(fn), timeit(tfn)
+        ms = timeit(fn)
+        tms = float("nan") if NOTORCH else timeit(tfn)
         out[f"{name}_{kind}"] = {"ms": round(ms, 4), "tflops": round(f / ms / 1e9, 1),
                                  "torch_f32_ms": round(tms, 4),
                                  "torch_tflops": round(f / tms / 1e9, 1)}

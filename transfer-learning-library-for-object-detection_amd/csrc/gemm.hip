@@ -387,6 +387,48 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
     }
     return;
   }
+  if ((size_t)(M + BM) * N * 4 < (1ull << 31)) {
+    // Branch-free (the conv epilogues' form, round 6): 32-bit byte offsets into C through a
+    // buffer resource; a row past M lies past the range (dropped store, zero load) and a
+    // column past N takes kBufOOB, so no element needs a bounds branch or a 64-bit address.
+    // Residual / mask operands of a 32-row block are loaded together ahead of its stores.
+    const unsigned bytes = (unsigned)M * (unsigned)N * 4u;
+    const i32x4 c_rsrc = make_buffer_rsrc(C, bytes);
+    const i32x4 r_rsrc = make_buffer_rsrc(res ? res : C, res ? bytes : 0u);
+    const i32x4 k_rsrc = make_buffer_rsrc(mask ? mask : C, mask ? bytes : 0u);
+#pragma unroll
+    for (int j = 0; j < kAccCols; ++j) {
+      const int n = n0 + wn * kNJ * 32 + acc_col(j, lane);
+      const float bv = bias != nullptr && n < N ? bias[n] : 0.f;
+      const int noff = n < N ? n * 4 : kBufOOB;
+#pragma unroll
+      for (int i = 0; i < acc_rows<MI>(); ++i) {
+        int off[kAccRegs];
+#pragma unroll
+        for (int r = 0; r < kAccRegs; ++r) {
+          const int m = m0 + wm * MI * 32 + acc_row(i, r, lane);
+          off[r] = noff == kBufOOB ? kBufOOB : m * N * 4 + noff;
+        }
+        float ext[kAccRegs], mk[kAccRegs];
+        if (res != nullptr || mask != nullptr) {
+#pragma unroll
+          for (int r = 0; r < kAccRegs; ++r) {
+            ext[r] = res != nullptr ? raw_buffer_load_f32(r_rsrc, off[r], 0, 0) : 0.f;
+            mk[r] = mask != nullptr ? raw_buffer_load_f32(k_rsrc, off[r], 0, 0) : 1.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < kAccRegs; ++r) {
+          float v = acc[i][j][r] + bv;
+          if (res != nullptr) v += ext[r];
+          if (relu) v = fmaxf(v, 0.f);
+          if (mask != nullptr) v = mk[r] > 0.f ? v : 0.f;
+          raw_buffer_store_f32(v, c_rsrc, off[r], 0, 0);
+        }
+      }
+    }
+    return;
+  }
   if (res == nullptr && !relu && mask == nullptr) {  // (plain: a short-K tile's cost is in it)
 #pragma unroll
     for (int j = 0; j < kAccCols; ++j) {

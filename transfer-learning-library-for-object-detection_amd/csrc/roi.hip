@@ -302,8 +302,10 @@ __global__ void rbg_start_kernel(const unsigned* __restrict__ keys, int n, unsig
   start[c] = lo;
 }
 
-// grid (R, ceil(C / 64)), 256 threads: sg[(r*S + s)*C + c]; thread (part = t / 64, channel
-// t % 64) writes samples part, part + 4, ... (a 256-B row of channels per sample and wave)
+// grid (R, ceil(C / 64)), 256 threads: sg[(r*S + s)*C + c].  V = 4 (C % 4 == 0): thread
+// (sample group t / 16, channel quad t % 16) writes 16-B stores, 16 lanes a 256-B row of one
+// sample; V = 1: thread (part t / 64, channel t % 64), a 256-B row per wave and sample
+template <int V>
 __global__ void __launch_bounds__(256) rbg_sample_grad_kernel(const float* __restrict__ top,
                                                               int C, int ph, int pw,
                                                               float* __restrict__ sg) {
@@ -314,16 +316,26 @@ __global__ void __launch_bounds__(256) rbg_sample_grad_kernel(const float* __res
   const float* tp = top + ((size_t)r * C + c0) * P;
   for (int e = t; e < nc * P; e += 256) g7[e] = tp[e] / 4.f;  // coalesced slab
   __syncthreads();
-  const int ch = t & 63;
+  constexpr int LPS = 64 / V;       // lanes per sample row
+  constexpr int SPI = 256 / LPS;    // samples per iteration
+  const int ch = (t % LPS) * V;
   if (ch >= nc) return;
-  const float* gp = g7 + ch * P;
   float* o = sg + (size_t)r * S * C + c0 + ch;
-  for (int smp = t >> 6; smp < S; smp += 4) {
+  for (int smp = t / LPS; smp < S; smp += SPI) {
     const int sy = smp / aw, sx = smp % aw;
-    float g = 0.f;  // avg_pool2d backward: py outer, px inner
-    for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
-      for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) g += gp[py * pw + px];
-    o[(size_t)smp * C] = g;
+    float g[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float* gp = g7 + (ch + v) * P;
+      float a = 0.f;  // avg_pool2d backward: py outer, px inner
+      for (int py = max(0, sy - 1); py <= min(sy, ph - 1); ++py)
+        for (int px = max(0, sx - 1); px <= min(sx, pw - 1); ++px) a += gp[py * pw + px];
+      g[v] = a;
+    }
+    if constexpr (V == 4)
+      *reinterpret_cast<float4*>(o + (size_t)smp * C) = make_float4(g[0], g[1], g[2], g[3]);
+    else
+      o[(size_t)smp * C] = g[0];
   }
 }
 
@@ -800,8 +812,12 @@ extern "C" int tlod_roi_align_avg_bwd_f32(const float* top_grad, int B, int C, i
     hipLaunchKernelGGL(rbg_start_kernel, dim3(div_up((int)ncell + 1, 256)), dim3(256), 0, s,
                        w.keys_s, n, ncell, w.start);
     TLOD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(rbg_sample_grad_kernel, dim3(R, div_up(C, 64)), dim3(256), 0, s, top_grad,
-                       C, ph, pw, w.sg);
+    if (C % 4 == 0)
+      hipLaunchKernelGGL(rbg_sample_grad_kernel<4>, dim3(R, div_up(C, 64)), dim3(256), 0, s,
+                         top_grad, C, ph, pw, w.sg);
+    else
+      hipLaunchKernelGGL(rbg_sample_grad_kernel<1>, dim3(R, div_up(C, 64)), dim3(256), 0, s,
+                         top_grad, C, ph, pw, w.sg);
     TLOD_LAUNCH_CHECK();
     TLOD_HIP(hipMemsetAsync(w.acc, 0, ncell_sz * C * sizeof(float), s));
     const int nseg = div_up(n, 64);
