@@ -358,6 +358,28 @@ int tlod_gemm_bs_mask_f32(const float* a, const float* b, const float* residual,
                           int b_kcontig, int nprod, void* ws, size_t ws_bytes,
                           tlod_stream_t stream);
 
+/* The ResNet RoI head's 3x3 conv (layer4's bottleneck conv2 on the RoIs' 4 x 4 maps,
+ * lib/DAF/resnet.py:66-102 via RCNN_top :286-288; the reference runs nn.Conv2d / cuDNN) as
+ * an implicit split-bf16 GEMM over channels-last maps: the (R H W) x 9 C im2col matrix, taps
+ * in (kh, kw, c) order with zero padding 1, is never materialised (it replaces
+ * tlod_im2col3x3_nhwc_f32 + tlod_gemm_bs_* and, for the input gradient,
+ * tlod_col2im3x3_nhwc_mask_f32).  Maps: R maps of H x W, channels-last rows (R H W, .).
+ *   mode 0 (forward):        c (R H W, O) = act(im2col(a) . b^T + bias (+ residual));
+ *                            a = x (R H W, C), b = the weight rows (O, 9 C) in (kh, kw, c)
+ *                            order; C % 16 == 0
+ *   mode 1 (input gradient): c (R H W, C) = (im2col(a) . b (+ residual)) * (mask > 0 if mask);
+ *                            a = dy (R H W, O), b = (9 O, C): row (t, o) = weight row o at tap
+ *                            8 - t (the flipped kernel); O % 16 == 0
+ *   mode 2 (weight grad):    c (O, 9 C) = a^T . im2col(b); a = dy (R H W, O), b = x; C % 256
+ *                            == 0; no epilogue (bias, residual, mask NULL, relu 0)
+ * Split-K pieces reduced in a fixed order (deterministic); workspace:
+ * tlod_gemm_nhwc3_bs_workspace_bytes(mode, ...). */
+size_t tlod_gemm_nhwc3_bs_workspace_bytes(int mode, int R, int H, int W, int C, int O, int nprod);
+int tlod_gemm_nhwc3_bs_f32(int mode, const float* a, const float* b, const float* bias,
+                           const float* residual, const float* mask, int relu, float* c, int R,
+                           int H, int W, int C, int O, int nprod, void* ws, size_t ws_bytes,
+                           tlod_stream_t stream);
+
 /* Split-bf16 3x3 convolution as an implicit GEMM over (c, tap) x flattened pixels, for
  * wide outputs (Cout >= 256): the forward of tlod_conv_fwd_ex_f32 (w_layout = 0: w is the
  * nn.Conv2d weight [Cout][Cin][3][3] as is) or the dgrad (w_layout = 1: w is

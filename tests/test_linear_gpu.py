@@ -140,3 +140,46 @@ def test_relu_dropout_p0_leaves_cpu_rng_alone():
     relu_dropout(torch.randn(64, device=dev), d)
     b = torch.rand(3)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("R,H,W,C,O", [(1, 4, 4, 256, 256), (37, 4, 4, 512, 512), (300, 4, 4, 256, 512),
+                                       (3, 5, 7, 256, 48), (2, 1, 3, 512, 16)])
+def test_gemm_nhwc3_modes(R, H, W, C, O):
+    """tlod_gemm_nhwc3_bs_f32: the RoI head's 3x3 conv as implicit GEMMs over channels-last
+    maps vs torch fp64 — forward with the bias / residual / ReLU epilogue, the input gradient
+    with the residual + ReLU-mask epilogue (through the tap-flipped weight), the weight
+    gradient; ragged map sizes (5 x 7, 1 x 3: every tap border), split-K tails (R = 1)."""
+    import torch.nn.functional as F
+    from tlod.linear import gemm_nhwc3
+    g = torch.Generator().manual_seed(R * 31 + C + O + W)
+    x = torch.randn(R, H, W, C, generator=g)
+    w = torch.randn(O, C, 3, 3, generator=g) * (2.0 / (9 * C)) ** 0.5
+    dy = torch.randn(R, H, W, O, generator=g)
+    bias, res = torch.randn(O, generator=g), torch.randn(R, H, W, O, generator=g)
+    xc = x.permute(0, 3, 1, 2).double()
+    wm = w.permute(0, 2, 3, 1).reshape(O, 9 * C)
+    rows = R * H * W
+    # forward (plain and with the full epilogue)
+    ref = F.conv2d(xc, w.double(), padding=1).permute(0, 2, 3, 1).reshape(rows, O)
+    y = gemm_nhwc3(0, x.reshape(rows, C).to(dev), wm.to(dev), R, H, W, C, O)
+    _close(y, ref, "bf16x6")
+    y = gemm_nhwc3(0, x.reshape(rows, C).to(dev), wm.to(dev), R, H, W, C, O, bias=bias.to(dev),
+                   residual=res.reshape(rows, O).to(dev), relu=True)
+    refe = torch.relu(ref + bias.double() + res.reshape(rows, O).double())
+    _close(y * (refe > 0).to(dev), refe, "bf16x6")  # (mask flips at f32 rounding of 0)
+    # input gradient
+    wd = wm.view(O, 9, C).flip(1).transpose(0, 1).reshape(9 * O, C)
+    refd = torch.nn.grad.conv2d_input(xc.shape, w.double(), dy.permute(0, 3, 1, 2).double(),
+                                      padding=1).permute(0, 2, 3, 1).reshape(rows, C)
+    dx = gemm_nhwc3(1, dy.reshape(rows, O).to(dev), wd.to(dev), R, H, W, C, O)
+    _close(dx, refd, "bf16x6")
+    m = torch.relu(torch.randn(rows, C, generator=g))
+    r2 = torch.randn(rows, C, generator=g)
+    dxm = gemm_nhwc3(1, dy.reshape(rows, O).to(dev), wd.to(dev), R, H, W, C, O,
+                     residual=r2.to(dev), mask=m.to(dev))
+    assert torch.equal(dxm, (dx + r2.to(dev)) * (m.to(dev) > 0))
+    # weight gradient, in the (O, 9C) GEMM layout
+    refw = torch.nn.grad.conv2d_weight(xc, (O, C, 3, 3), dy.permute(0, 3, 1, 2).double(),
+                                       padding=1).permute(0, 2, 3, 1).reshape(O, 9 * C)
+    dw = gemm_nhwc3(2, dy.reshape(rows, O).to(dev), x.reshape(rows, C).to(dev), R, H, W, C, O)
+    _close(dw, refw, "bf16x6")

@@ -176,8 +176,9 @@ def test_head_fused_backward_bit_identical(R, entry, monkeypatch):
     x = torch.randn(R, H, H, 1024, generator=g).to(dev)
     gy = torch.randn(R, 2048, generator=g).to(dev)
 
-    def run(fuse):
+    def run(fuse, implicit="0"):
         monkeypatch.setenv("TLOD_HEAD_FUSE", fuse)
+        monkeypatch.setenv("TLOD_HEAD_IMPLICIT", implicit)
         for p in top.parameters():
             p.grad = None
         xi = x.clone().requires_grad_(True)
@@ -191,6 +192,18 @@ def test_head_fused_backward_bit_identical(R, entry, monkeypatch):
     plain = run("0")
     for i, (a, b) in enumerate(zip(fused, plain)):
         assert torch.equal(a, b), i
+    # round 6: conv2 as implicit GEMMs over the map (the default).  The forward and conv2's
+    # weight gradient take the same K order as the im2col GEMMs: bit for bit; the input
+    # gradient sums its 9 x 512 products in one GEMM instead of a GEMM + col2im's 9-tap sum,
+    # so every gradient upstream of it agrees to f32 rounding
+    before = dict(linear.STATS)
+    impl = run("1", "1")
+    assert linear.STATS["masked_dgrad"] - before["masked_dgrad"] == 8  # + 3 x conv2's input grad
+    assert linear.STATS["relu_bwd_skipped"] - before["relu_bwd_skipped"] == 8
+    assert torch.equal(impl[0], plain[0])
+    for i, (a, b) in enumerate(zip(impl[1:], plain[1:])):
+        err = float((a.double() - b.double()).norm() / b.double().norm())
+        assert err < 1e-5, (i, err)
 
 
 @pytest.mark.parametrize("entry", [True, False])

@@ -161,6 +161,102 @@ struct Stager {
   }
 };
 
+// Implicit im2col of channels-last 3x3 / pad-1 maps (the ResNet RoI head's conv2, round 6):
+// rows m = (r, h, w) of R maps of H x W with Cimg channels; column (tap, c), tap = 3 kh + kw,
+// reads X[m + (kh - 1) W + (kw - 1)][c], 0 outside the map (its RoI's 4 x 4 bins).  The
+// (R H W) x 9 Cimg matrix the head materialised (im2col3x3_nhwc, then col2im3x3_nhwc for
+// its gradient) is never written.
+//  * NhwcStagerK: the K-contiguous operand A(m, k = tap Cimg + c) (Cimg % 16 == 0: a 16-deep
+//    chunk lies in one tap);
+//  * NhwcStagerN: the N-contiguous operand B(n = tap Cimg + c, k = m) of the weight gradient
+//    (Cimg % 256 == 0: a 256-wide column tile lies in one tap).
+struct NhwcGeom {
+  int H, W, C, rows;  // map rows x columns, channels, R H W
+};
+template <int NPL, int RT>
+struct NhwcStagerK : Stager<1, NPL, RT> {
+  using Base = Stager<1, NPL, RT>;
+  int rm[Base::IT], rh[Base::IT], rw[Base::IT];  // the lane's tile rows m (-1: none), h, w
+  NhwcGeom g;
+  __device__ void init(const float* P, NhwcGeom g_, int r0, int tid) {
+    g = g_;
+    this->rsrc = make_buffer_rsrc(P, (unsigned)g.rows * (unsigned)g.C * 4u);
+    this->ktot = 9 * g.C;
+    this->tid0 = tid;
+#pragma unroll
+    for (int i = 0; i < Base::IT; ++i) {
+      const int idx = tid + i * kNT;
+      const bool slot = idx < Base::VECS;
+      const int row = idx >> 2, k4 = (idx & 3) * 4;
+      const int m = r0 + row;
+      rm[i] = slot && m < g.rows ? m : -1;
+      rh[i] = (m % (g.H * g.W)) / g.W;
+      rw[i] = m % g.W;
+      this->off[i] = k4;
+      this->lds[i] = slot ? kimg_off(row, k4 >> 3) + 2 * (k4 & 7) : -1;
+      this->lim[i] = 1 << 30;
+    }
+  }
+  template <int S = 0>
+  __device__ void load(int kc, int) {
+    f32x4v* rr = S ? this->r2 : this->r;
+    unsigned* mm = S ? this->mask2 : this->mask;
+    this->kb[S] = kc;
+    const int tap = kc / g.C, cc = kc - tap * g.C;
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < Base::IT; ++i) {
+      const bool ok = rm[i] >= 0 && (unsigned)(rh[i] + dh) < (unsigned)g.H &&
+                      (unsigned)(rw[i] + dw) < (unsigned)g.W && kc < 9 * g.C;
+      rr[i] = raw_buffer_load_v4f32(
+          this->rsrc, ok ? ((rm[i] + dh * g.W + dw) * g.C + cc + this->off[i]) * 4 : kBufOOB, 0, 0);
+      mm[i] = 0xfu;
+    }
+  }
+};
+template <int NPL, int RT>
+struct NhwcStagerN : Stager<0, NPL, RT> {
+  using Base = Stager<0, NPL, RT>;
+  int kr[Base::IT], cb[Base::IT];  // the lane's k row in the chunk (-1: none), channel
+  int dh, dw;                      // the column tile's tap
+  NhwcGeom g;
+  __device__ void init(const float* P, NhwcGeom g_, int n0, int tid) {
+    g = g_;
+    this->rsrc = make_buffer_rsrc(P, (unsigned)g.rows * (unsigned)g.C * 4u);
+    this->tid0 = tid;
+    const int tap = n0 / g.C;
+    dh = tap / 3 - 1;
+    dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < Base::IT; ++i) {
+      const int idx = tid + i * kNT;
+      const bool slot = idx < Base::VECS;
+      const int k = idx / Base::LPR, c4 = (idx % Base::LPR) * 4;
+      kr[i] = slot ? k : -1;
+      cb[i] = n0 - tap * g.C + c4;
+      this->lds[i] = slot ? k * kPitchMN + 2 * c4 : -1;
+      this->off[i] = 0;
+      this->lim[i] = 4;
+    }
+  }
+  template <int S = 0>
+  __device__ void load(int kc, int) {
+    f32x4v* rr = S ? this->r2 : this->r;
+    unsigned* mm = S ? this->mask2 : this->mask;
+    this->kb[S] = kc;
+#pragma unroll
+    for (int i = 0; i < Base::IT; ++i) {
+      const int m = kc + kr[i];
+      const int h = (m % (g.H * g.W)) / g.W, w = m % g.W;
+      const bool ok = kr[i] >= 0 && m < g.rows && (unsigned)(h + dh) < (unsigned)g.H &&
+                      (unsigned)(w + dw) < (unsigned)g.W;
+      rr[i] = raw_buffer_load_v4f32(
+          this->rsrc, ok ? ((m + dh * g.W + dw) * g.C + cb[i]) * 4 : kBufOOB, 0, 0);
+      mm[i] = 0xfu;
+    }
+  }
+};
+
 // MFMA operand (8 k values of row/column `base + l32`) from one plane image.
 template <int KC>
 __device__ __forceinline__ u32x4 read_operand(const unsigned char* img, int base, int lane) {
@@ -332,12 +428,14 @@ __device__ __forceinline__ void mainloop(SA& sa, SB& sb, Acc<MI>& acc_, int c_be
   }
 }
 
-template <int AK, int BK, int NP, int MI>
+// IM: 0 = plain operands; 1 = A is the implicit channels-last 3x3 im2col of geo's maps
+// (NhwcStagerK); 2 = B is (NhwcStagerN)
+template <int AK, int BK, int NP, int MI, int IM = 0>
 __global__ void __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
                const float* __restrict__ bias, const float* __restrict__ res, int relu,
                const float* __restrict__ mask, float* __restrict__ C, float* __restrict__ slab, int M, int N, int K, int tiles_m,
-               int tiles_n, int dp_tiles, int ksplit, int chunks_per_split) {
+               int tiles_n, int dp_tiles, int ksplit, int chunks_per_split, NhwcGeom geo) {
   constexpr int NPL = NP == 6 ? 3 : 2;
   constexpr int BM = kWM * MI * 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -364,12 +462,26 @@ gemm_bs_kernel(const float* __restrict__ A, const float* __restrict__ B,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / kWN, wn = wid % kWN;
 
-  Stager<AK, NPL, BM> sa;
-  Stager<BK, NPL, kBN> sb;
-  sa.init(A, M, K, m0, tid);
-  sb.init(B, N, K, n0, tid);
   Acc<MI> acc_;
-  mainloop<AK, BK, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, M, N);
+  if constexpr (IM == 1) {
+    NhwcStagerK<NPL, BM> sa;
+    Stager<BK, NPL, kBN> sb;
+    sa.init(A, geo, m0, tid);
+    sb.init(B, N, K, n0, tid);
+    mainloop<AK, BK, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, M, N);
+  } else if constexpr (IM == 2) {
+    Stager<AK, NPL, BM> sa;
+    NhwcStagerN<NPL, kBN> sb;
+    sa.init(A, M, K, m0, tid);
+    sb.init(B, geo, n0, tid);
+    mainloop<AK, BK, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, M, N);
+  } else {
+    Stager<AK, NPL, BM> sa;
+    Stager<BK, NPL, kBN> sb;
+    sa.init(A, M, K, m0, tid);
+    sb.init(B, N, K, n0, tid);
+    mainloop<AK, BK, NP, MI>(sa, sb, acc_, c_begin, c_end, smem, M, N);
+  }
   auto& acc = acc_.t;
 
   // direct tiles: C = act(acc + bias + res); tail pieces: tile-local slab (the epilogue is
@@ -567,13 +679,13 @@ TailPlan plan_tail(int T, int nchunks, int slots, double tile_s, double tile_byt
   return p;
 }
 
-template <int AK, int BK, int NP, int MI>
+template <int AK, int BK, int NP, int MI, int IM = 0>
 struct Gemm {
   static constexpr int NPL = NP == 6 ? 3 : 2;
   static constexpr int kBM = kWM * MI * 32;
   static constexpr size_t kLds = 2 * NPL * (Img<AK, kBM>::PLANE + Img<BK>::PLANE);
   static TailPlan plan(int M, int N, int K) {
-    const int slots = slots_of(gemm_bs_kernel<AK, BK, NP, MI>, kLds);
+    const int slots = slots_of(gemm_bs_kernel<AK, BK, NP, MI, IM>, kLds);
     const int tiles = div_up(M, kBM) * div_up(N, kBN);
     const int nchunks = div_up(K, kTK);
     // bf16 MFMA time of one whole tile per resident slot at ~50% of the dense peak
@@ -587,7 +699,7 @@ struct Gemm {
   }
   static int run(const float* A, const float* B, const float* bias, float* C, int M, int N, int K,
                  float* ws, size_t ws_bytes_, hipStream_t s, const float* res = nullptr,
-                 int relu = 0, const float* mask = nullptr) {
+                 int relu = 0, const float* mask = nullptr, NhwcGeom geo = NhwcGeom{0, 0, 0, 0}) {
     const TailPlan p = plan(M, N, K);
     if (ws_bytes_ < ws_bytes(M, N, K)) {
       set_error("tlod_gemm_bs_f32: workspace too small");
@@ -595,11 +707,11 @@ struct Gemm {
     }
     const int tiles_m = div_up(M, kBM), tiles_n = div_up(N, kBN);
     const int n_tail = tiles_m * tiles_n - p.dp_tiles;
-    auto kern = gemm_bs_kernel<AK, BK, NP, MI>;
+    auto kern = gemm_bs_kernel<AK, BK, NP, MI, IM>;
     TLOD_HIP(lds_attr((const void*)kern, (int)kLds));
     const int nwg = p.dp_tiles + (p.ksplit > 1 ? n_tail * p.ksplit : 0);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(kNT), kLds, s, A, B, bias, res, relu, mask, C, ws, M,
-                       N, K, tiles_m, tiles_n, p.dp_tiles, p.ksplit, p.cps);
+                       N, K, tiles_m, tiles_n, p.dp_tiles, p.ksplit, p.cps, geo);
     TLOD_LAUNCH_CHECK();
     if (p.ksplit > 1) {
       hipLaunchKernelGGL(gemm_tail_reduce_kernel, dim3(n_tail * (kBM * kBN / 1024)), dim3(256), 0,
@@ -627,6 +739,34 @@ auto with_gemm(int M, int ak, int bk, int nprod, F&& f) {
   // (0, 1): the callers pass 0/1 flags, so the four cases are exhaustive
   if (m192) return nprod == 6 ? f(Gemm<0, 1, 6, 3>{}) : f(Gemm<0, 1, 3, 3>{});
   return nprod == 6 ? f(Gemm<0, 1, 6, 4>{}) : f(Gemm<0, 1, 3, 4>{});
+}
+
+// The channels-last 3x3 GEMM of a mode (tlod_gemm_nhwc3_bs_f32): 0 forward (A implicit,
+// B the (O, 9C) weight rows), 1 input gradient (A implicit over dY's O channels, B the
+// (9 O, C) tap-flipped weight), 2 weight gradient (A = dY^T, B implicit); the M tile as
+// with_gemm.
+template <typename F>
+auto with_nhwc3(int mode, int M, int nprod, F&& f) {
+  const bool m192 = div_up(M, 192) * 192 < div_up(M, 256) * 256;
+#define TLOD_NHWC3_CASE(A_, B_, IM_)                                                      \
+  if (m192) return nprod == 6 ? f(Gemm<A_, B_, 6, 3, IM_>{}) : f(Gemm<A_, B_, 3, 3, IM_>{}); \
+  return nprod == 6 ? f(Gemm<A_, B_, 6, 4, IM_>{}) : f(Gemm<A_, B_, 3, 4, IM_>{});
+  if (mode == 0) { TLOD_NHWC3_CASE(1, 1, 1) }
+  if (mode == 1) { TLOD_NHWC3_CASE(1, 0, 1) }
+  TLOD_NHWC3_CASE(0, 0, 2)
+#undef TLOD_NHWC3_CASE
+}
+
+struct Nhwc3Shape {
+  int M, N, K;
+  NhwcGeom geo;
+};
+// GEMM extents and the implicit operand's geometry of a mode (see tlod.h)
+static Nhwc3Shape nhwc3_shape(int mode, int R, int H, int W, int C, int O) {
+  const int rows = R * H * W;
+  if (mode == 0) return {rows, O, 9 * C, NhwcGeom{H, W, C, rows}};
+  if (mode == 1) return {rows, C, 9 * O, NhwcGeom{H, W, O, rows}};
+  return {O, 9 * C, rows, NhwcGeom{H, W, C, rows}};
 }
 
 // ---------------------------------------------------------------- 3x3 conv as GEMM
@@ -1102,5 +1242,38 @@ extern "C" int tlod_conv1x1_gemm_bs_f32(const float* x, const float* w, int w_la
   return with_conv1x1_gemm(w_layout, nprod, N, H, W, Cout, [&](auto g) {
     return g.run(x, w, ConvEpi{scale, bias, residual, relu}, y, N, Cin, H, W, Cout,
                  static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+  });
+}
+
+extern "C" size_t tlod_gemm_nhwc3_bs_workspace_bytes(int mode, int R, int H, int W, int C, int O,
+                                                    int nprod) {
+  if (mode < 0 || mode > 2 || R <= 0 || H <= 0 || W <= 0 || C <= 0 || O <= 0 ||
+      (nprod != 3 && nprod != 6))
+    return 0;
+  const Nhwc3Shape sh = nhwc3_shape(mode, R, H, W, C, O);
+  return with_nhwc3(mode, sh.M, nprod, [&](auto g) { return g.ws_bytes(sh.M, sh.N, sh.K); });
+}
+
+extern "C" int tlod_gemm_nhwc3_bs_f32(int mode, const float* a, const float* b, const float* bias,
+                                      const float* residual, const float* mask, int relu,
+                                      float* c, int R, int H, int W, int C, int O, int nprod,
+                                      void* ws, size_t ws_bytes, tlod_stream_t stream) {
+  TLOD_CHECK_ARG(mode >= 0 && mode <= 2, "mode must be 0 (forward), 1 (input gradient) or 2");
+  TLOD_CHECK_ARG(R > 0 && H > 0 && W > 0 && C > 0 && O > 0 && a && b && c, "bad arguments");
+  TLOD_CHECK_ARG(nprod == 3 || nprod == 6, "nprod must be 3 or 6");
+  TLOD_CHECK_ARG(mode == 0 ? C % 16 == 0 : mode == 1 ? O % 16 == 0 : C % 256 == 0,
+                 "channel count: the implicit operand's chunks / tiles must not straddle taps");
+  TLOD_CHECK_ARG(mode != 2 || (bias == nullptr && residual == nullptr && mask == nullptr && !relu),
+                 "the weight gradient takes no epilogue");
+  TLOD_CHECK_ARG(residual != c && mask != c, "residual / mask must not alias c");
+  const Nhwc3Shape sh = nhwc3_shape(mode, R, H, W, C, O);
+  // 32-bit buffer byte offsets (the implicit operand: rows x channels; the weights: 9 C O)
+  TLOD_CHECK_ARG((size_t)sh.geo.rows * std::max(C, O) * 4 < (1ull << 31) &&
+                     (size_t)9 * C * O * 4 < (1ull << 31) &&
+                     (size_t)std::max(sh.M, sh.N) * sh.K * 4 < (1ull << 31),
+                 "operand too large");
+  return with_nhwc3(mode, sh.M, nprod, [&](auto g) {
+    return g.run(a, b, bias, c, sh.M, sh.N, sh.K, static_cast<float*>(ws), ws_bytes,
+                 (hipStream_t)stream, residual, relu, mask, sh.geo);
   });
 }

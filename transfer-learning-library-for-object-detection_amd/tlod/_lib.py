@@ -170,6 +170,10 @@ SIGNATURES = {
     "tlod_subsample2_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_upsample2_zero_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_im2col3x3_nhwc_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "tlod_gemm_nhwc3_bs_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int,
+                                                      c_int]),
+    "tlod_gemm_nhwc3_bs_f32": (c_int, [c_int, P, P, P, P, P, c_int, P, c_int, c_int, c_int, c_int,
+                                       c_int, c_int, P, c_size_t, P]),
     "tlod_col2im3x3_nhwc_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "tlod_col2im3x3_nhwc_mask_f32": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "tlod_image_blob_u8": (c_int, [P, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,

@@ -180,12 +180,14 @@ class Bottleneck(nn.Module):
     # ---------------------------------------------------------------- RoI head path
     @staticmethod
     def _gemm_bn(xm, conv, bn, relu, residual=None, relu_in=False, link=None, role=0,
-                 mean_hw=None):
+                 mean_hw=None, nhwc3=None):
         """xm: (P, Cin) channels-last rows; conv as a GEMM + folded BN (+res) (+ReLU).
         relu_in: xm is a ReLU output (its input gradient is masked in the GEMM epilogue);
         link / role: the identity shortcut's gradient handed from conv3 (role 3) to conv1
         (role 1) — see LinearActFunction.  mean_hw = (R, H, W): return the head's spatial
-        mean (R, Cout) instead of the rows (split-bf16 path only; the caller checks)."""
+        mean (R, Cout) instead of the rows (split-bf16 path only; the caller checks).
+        nhwc3 = (R, H, W): conv is 3x3 and xm its input map's rows, not the im2col matrix
+        (the implicit GEMMs; split-bf16 path only, the caller checks)."""
         scale, shift = fold_bn(bn)
         w = conv.weight
         wm = w.view(w.shape[0], -1) if w.shape[2] == 1 else w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
@@ -204,7 +206,7 @@ class Bottleneck(nn.Module):
         with torch.no_grad():
             wf = (wm * scale[:, None]).contiguous()
         return LinearActFunction.apply(xm.contiguous(), wf, shift, residual, relu, m, relu_in,
-                                       link, role, w, scale, mean_hw)
+                                       link, role, w, scale, mean_hw, nhwc3)
 
     def forward_nhwc(self, x, subsampled=False, shape=None, relu_in=False, mean=False):
         """The layer4 RoI head, channels-last.  x: (R, H, W, C), or (R*H*W, C) rows with
@@ -230,8 +232,14 @@ class Bottleneck(nn.Module):
                             link=link, role=1)
         P = out.shape[1]
         self._tap("r1", out.view(R, H, W, P), nhwc=True)
-        taps = im2col3x3_nhwc(out, (R, H, W), relu_in=fused)
-        out = self._gemm_bn(taps, self.conv2, self.bn2, relu=True)
+        if fused and P % 256 == 0 and _lib.env("TLOD_HEAD_IMPLICIT", "1") != "0":
+            # conv2 as implicit GEMMs over the channels-last map (no im2col / col2im passes);
+            # conv1's ReLU backward runs in conv2's input-gradient epilogue (relu_in)
+            out = self._gemm_bn(out, self.conv2, self.bn2, relu=True, relu_in=True,
+                                nhwc3=(R, H, W))
+        else:
+            taps = im2col3x3_nhwc(out, (R, H, W), relu_in=fused)
+            out = self._gemm_bn(taps, self.conv2, self.bn2, relu=True)
         self._tap("r2", out.view(R, H, W, P), nhwc=True)
         res = (self._gemm_bn(xm, self.downsample[0], self.downsample[1], relu=False,
                              link=link, role=4)

@@ -117,6 +117,37 @@ def gemm_mask(a, b, M, N, K, a_kcontig, b_kcontig, mask, residual=None, math="bf
     return c
 
 
+def gemm_nhwc3(mode, a, b, R, H, W, C, O, bias=None, residual=None, mask=None, relu=False,
+               math="bf16x6", out=None):
+    """The RoI head's 3x3 conv as an implicit GEMM over channels-last (R*H*W, .) rows
+    (tlod_gemm_nhwc3_bs_f32): mode 0 forward (a = x, b = the (O, 9C) weight rows), 1 input
+    gradient (a = dy, b = the (9O, C) flipped weight; mask: the input's ReLU output, the
+    result tagged as masked), 2 weight gradient (a = dy, b = x) -> (O, 9C)."""
+    a, b = a.contiguous(), b.contiguous()
+    nprod = 6 if math == "bf16x6" else 3
+    L = _lib.lib()
+    rows = R * H * W
+    shape = {0: (rows, O), 1: (rows, C), 2: (O, 9 * C)}[mode]
+    c = torch.empty(shape, dtype=torch.float32, device=a.device) if out is None else out
+    assert c.is_contiguous() and c.numel() == shape[0] * shape[1]
+    ws = _lib.workspace(L.tlod_gemm_nhwc3_bs_workspace_bytes(mode, R, H, W, C, O, nprod),
+                        a.device, "gemm")
+    bias = bias.detach().contiguous() if bias is not None else None
+    residual = residual.detach().contiguous() if residual is not None else None
+    mask = mask.detach().contiguous() if mask is not None else None
+    from .conv import _timed
+    mnk = {0: (rows, O, 9 * C), 1: (rows, C, 9 * O), 2: (O, 9 * C, rows)}[mode]
+    _timed("gemm", mnk, lambda: _lib.check(
+        L.tlod_gemm_nhwc3_bs_f32(mode, _lib.ptr(a), _lib.ptr(b), _lib.ptr(bias),
+                                 _lib.ptr(residual), _lib.ptr(mask), int(relu), _lib.ptr(c), R, H,
+                                 W, C, O, nprod, _lib.ptr(ws), ws.numel(), _lib.stream_of(a)),
+        "gemm_nhwc3_bs"), math)
+    if mask is not None:
+        c._tlod_relu_masked = (mask.data_ptr(), c.data_ptr(), c._version)
+        STATS["masked_dgrad"] += 1
+    return c
+
+
 STATS = {"masked_dgrad": 0, "relu_bwd_skipped": 0}  # fused ReLU-backward counters (tests)
 
 
@@ -135,14 +166,22 @@ class LinearActFunction(torch.autograd.Function):
     form of wsrc * wscale (rows (kh, kw, c) for 3x3), computed by the caller without autograd;
     the backward writes d wsrc = (dy^T x in the GEMM form) * wscale, re-laid out, straight
     into wsrc's gradient slot (one pass) instead of autograd's mul, permute copy and the
-    arena's copy of the result."""
+    arena's copy of the result.
+    nhwc3 = (R, H, W) (round 6): x is not the im2col matrix of a 3x3 conv but its channels-last
+    input map rows (R*H*W, C), and weight the (O, 9C) rows — the three GEMMs run as implicit
+    GEMMs over the map (gemm_nhwc3: no im2col / col2im passes, no (R*H*W, 9C) tensor saved)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, relu, math, relu_in=False, link=None, role=0,
-                wsrc=None, wscale=None, mean_hw=None):
+                wsrc=None, wscale=None, mean_hw=None, nhwc3=None):
         R, I = x.shape
         O = weight.shape[0]
-        y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math, residual=residual, relu=relu)
+        ctx.nhwc3 = nhwc3
+        if nhwc3 is not None:
+            y = gemm_nhwc3(0, x, weight.detach(), *nhwc3, I, O, bias=bias, residual=residual,
+                           relu=relu, math=math)
+        else:
+            y = gemm(x, weight.detach(), R, O, I, 1, 1, bias, math, residual=residual, relu=relu)
         ctx.mean_hw = mean_hw
         ctx.math, ctx.relu = math, relu
         ctx.has_bias, ctx.has_res = bias is not None, residual is not None
@@ -184,20 +223,32 @@ class LinearActFunction(torch.autograd.Function):
             res, ctx.link.g = ctx.link.g, None
             ctx.link.consumed = True  # a role-4 backward running later returns its own dx
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            if ctx.relu_in:
-                dx = gemm_mask(g, weight.detach(), R, I, O, 1, 0, x, res, ctx.math)
-            else:
-                dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math, residual=res)
+        n3 = ctx.nhwc3
+        if n3 is not None:  # implicit 3x3 GEMMs over the map (I = C channels here)
+            def wgrad(out=None):
+                return gemm_nhwc3(2, g, x, *n3, I, O, math=ctx.math, out=out)
+            if ctx.needs_input_grad[0]:
+                with torch.no_grad():  # row (t, o) = weight row o at tap 8 - t
+                    wd = weight.detach().view(O, 9, I).flip(1).transpose(0, 1).reshape(9 * O, I)
+                dx = gemm_nhwc3(1, g, wd, *n3, I, O, residual=res,
+                                mask=x if ctx.relu_in else None, math=ctx.math)
+        else:
+            def wgrad(out=None):
+                return gemm(g, x, O, I, R, 0, 0, None, ctx.math, out=out)
+            if ctx.needs_input_grad[0]:
+                if ctx.relu_in:
+                    dx = gemm_mask(g, weight.detach(), R, I, O, 1, 0, x, res, ctx.math)
+                else:
+                    dx = gemm(g, weight.detach(), R, I, O, 1, 0, None, ctx.math, residual=res)
         if ctx.needs_input_grad[1]:
-            dw = gemm(g, x, O, I, R, 0, 0, None, ctx.math, out=grad_out(ctx.params[0]))
+            dw = wgrad(out=grad_out(ctx.params[0]))
         if (dx is not None and ctx.role == 4 and ctx.link is not None
                 and not getattr(ctx.link, "consumed", False)):
             ctx.link.g, dx = dx, None  # to conv1's input-gradient GEMM (role 1)
         dsrc = None
         if ctx.wsrc is not None and ctx.needs_input_grad[9]:
             w = ctx.wsrc
-            dwg = gemm(g, x, O, I, R, 0, 0, None, ctx.math)  # (O, I) in the GEMM layout
+            dwg = wgrad()  # (O, I) in the GEMM layout (3x3: (O, 9C))
             slot = grad_out(w)
             dsrc = slot if slot is not None else torch.empty_like(w)
             sc = ctx.wscale.detach()
@@ -213,7 +264,7 @@ class LinearActFunction(torch.autograd.Function):
         dres = g if ctx.has_res and ctx.needs_input_grad[3] else None
         if dres is not None and ctx.role == 3 and ctx.link is not None:
             ctx.link.g, dres = dres, None  # to conv1's backward
-        return dx, dw, db, dres, None, None, None, None, None, dsrc, None, None
+        return dx, dw, db, dres, None, None, None, None, None, dsrc, None, None, None
 
 
 class Linear(nn.Linear):
