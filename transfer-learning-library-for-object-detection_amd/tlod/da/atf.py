@@ -30,7 +30,7 @@ from ..config import cfg
 from ..rpn.proposal import proposals_on_side_streams
 from ..detector.losses import smooth_l1_loss, weighted_loss_sum
 from ..rpn.rpn_head import _RPN
-from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, image_label
+from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, early_rpn, early_rpn_backward, image_label
 from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
 from ..detector.vgg16 import VGG16_SPLITS
@@ -89,6 +89,7 @@ class _fasterRCNN(_DAFBase):
         gt_boxes = gt_boxes.detach()
         same = (im_data.shape == tgt_im_data.shape) and batch_size == 1
         rpn = self.RCNN_rpn
+        early = early_rpn(self, same)
 
         # ---- backbones: frozen conv1/conv2 are shared by both branches (vgg16.py:46-47)
         if same:
@@ -97,7 +98,10 @@ class _fasterRCNN(_DAFBase):
             c3_t, c4_t, base_t = self._branch(self.RCNN_base_t, z[:1])
             base_feat, tgt_base_feat = bs[:1], bs[1:]
             tgt_c3, tgt_c4 = c3s[1:], c4s[1:]
-            heads = rpn.head(torch.cat([base_feat, base_t, tgt_base_feat], 0))
+            rpn_in = torch.cat([base_feat, base_t, tgt_base_feat], 0)
+            if early:
+                rpn_in = rpn_in.detach().requires_grad_(True)
+            heads = rpn.head(rpn_in)
             hs = [tuple(h[i:i + 1] for h in heads) for i in range(3)]
         else:
             z = self._shared(im_data)
@@ -121,6 +125,10 @@ class _fasterRCNN(_DAFBase):
                                        rng=self.replay_rng)
         rpn_loss_cls = l_cls1 + l_cls2
         rpn_loss_bbox = l_box1 + l_box2
+        if early:  # rpn_in rows: source (RCNN_base), source (RCNN_base_t), target (RCNN_base)
+            rpn_loss_cls, rpn_loss_bbox = early_rpn_backward(
+                rpn_loss_cls, rpn_loss_bbox, rpn_in,
+                [(bs, lambda g: torch.cat([g[0:1], g[2:3]], 0)), (base_t, lambda g: g[1:2])])
         rois_domain, rois_domain_t, tgt_rois = pending.join()
         if self.capture is not None:
             self.capture.update(s_rois=rois_domain.detach().clone(),

@@ -112,6 +112,36 @@ class _InstanceDA(nn.Module):
         return x, instance_label(x.shape[0], need_backprop)
 
 
+
+def early_rpn(model, same):
+    """Early RPN backward (round 6): the RPN losses do not depend on the proposals, so their
+    backward (RPN head + RPN_Conv weight / input gradients) can run on the main stream while
+    the proposal layers' NMS runs on the side streams — the window in which the main stream
+    otherwise waits at pending.join() with the chip nearly idle.  The RPN head then reads a
+    detached copy of its input, and early_rpn_backward adds the input gradient to the
+    features' gradients by hooks in the main backward.  The returned RPN losses are detached
+    (their gradient, at weight 1 as in the reference's loss sums, methods/DAF/DAF_train.py:
+    397-400, MAF_train.py:415-418, ATF_train.py:405-408, is already in the RPN parameters' .grad): a caller that weights them differently
+    or runs a training forward without its backward sets TLOD_EARLY_RPN=0 (one backward).
+    Only on the batched (same-shape, batch 1) path."""
+    return (same and model.training and torch.is_grad_enabled()
+            and _lib.env("TLOD_EARLY_RPN", "1") != "0")
+
+
+def early_rpn_backward(loss_cls, loss_bbox, rpn_in, targets):
+    """Backpropagates the RPN losses now.  rpn_in: the detached leaf the RPN head read;
+    targets: (feature, share) pairs — share(rpn_in.grad) is the part of that gradient which
+    belongs to the feature (a slice / concatenation of rows), added to the feature's gradient
+    when the main backward reaches it.  Returns the detached losses."""
+    torch.autograd.backward(loss_cls + loss_bbox)
+    g = rpn_in.grad
+    if g is not None:
+        for feat, share in targets:
+            if feat.requires_grad:
+                gs = share(g)
+                feat.register_hook(lambda gf, gs=gs: gf + gs)
+    return loss_cls.detach(), loss_bbox.detach()
+
 class _fasterRCNN(nn.Module):
     """lib/DAF/faster_rcnn.py:22-247."""
 
@@ -183,18 +213,7 @@ class _fasterRCNN(nn.Module):
         im_info = im_info.detach()
         gt_boxes = gt_boxes.detach()
         same = (im_data.shape == tgt_im_data.shape) and batch_size == 1
-        # Early RPN backward (round 6): the RPN losses do not depend on the proposals, so
-        # their backward (RPN head + RPN_Conv weight / input gradients) runs on this stream
-        # while the proposal layers' NMS runs on the side streams — the window in which this
-        # stream otherwise waits at pending.join() with the chip nearly idle.  The RPN branch
-        # reads a detached copy of the base feature; its input gradient is added to the base
-        # feature's gradient by a hook in the main backward.  The returned RPN losses are
-        # then detached (their gradient, at weight 1 as in methods/DAF/DAF_train.py's loss
-        # sum, is already in the RPN parameters' .grad): a caller that weights them
-        # differently or runs a forward without its backward sets TLOD_EARLY_RPN=0.
-        # A/B (round 6, one lease): DAF-VGG16 75.6 vs 74.7 img/s.  TLOD_EARLY_RPN=0: one backward.
-        early = (same and self.training and torch.is_grad_enabled()
-                 and _lib.env("TLOD_EARLY_RPN", "1") != "0")
+        early = early_rpn(self, same)
         if same:
             base2 = self.RCNN_base(torch.cat([im_data, tgt_im_data], 0))
             base_feat, tgt_base_feat = base2[:1], base2[1:]
@@ -223,11 +242,8 @@ class _fasterRCNN(nn.Module):
             rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes,
                                                         im_info, num_boxes, rng=self.replay_rng)
         if early:
-            torch.autograd.backward(rpn_loss_cls + rpn_loss_bbox)
-            g_rpn = rpn_in.grad
-            if g_rpn is not None and base2.requires_grad:
-                base2.register_hook(lambda g: g + g_rpn)
-            rpn_loss_cls, rpn_loss_bbox = rpn_loss_cls.detach(), rpn_loss_bbox.detach()
+            rpn_loss_cls, rpn_loss_bbox = early_rpn_backward(
+                rpn_loss_cls, rpn_loss_bbox, rpn_in, [(base2, lambda g: g)])
         if same:
             score_img2 = self.RCNN_imageDA.score(base2)
         rois, tgt_rois = pending.join()

@@ -21,7 +21,7 @@ from ..conv import Conv2d
 from ..detector.losses import weighted_loss_sum
 from ..linear import Linear
 from ..rpn.proposal import proposals_on_side_streams
-from .daf import _ImageDA, _fasterRCNN as _DAFBase, grad_reverse, image_label
+from .daf import _ImageDA, _fasterRCNN as _DAFBase, early_rpn, early_rpn_backward, grad_reverse, image_label
 from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
 from ..detector.vgg16 import VGG16_SPLITS
@@ -224,10 +224,12 @@ class _fasterRCNN(_DAFBase):
         im_info = im_info.detach()
         gt_boxes = gt_boxes.detach()
         same = (im_data.shape == tgt_im_data.shape) and batch_size == 1
+        early = early_rpn(self, same)
         if same:
             c3, c4, base = self._backbone(torch.cat([im_data, tgt_im_data], 0))
             feats = [(c3, c4, base)]
-            score2, score_r2, prob2, bbox2 = self.RCNN_rpn.head(base)
+            rpn_in = base.detach().requires_grad_(True) if early else base
+            score2, score_r2, prob2, bbox2 = self.RCNN_rpn.head(rpn_in)
             s_score, s_score_r, s_prob, s_bbox = score2[:1], score_r2[:1], prob2[:1], bbox2[:1]
             t_prob, t_bbox = prob2[1:], bbox2[1:]
         else:
@@ -242,6 +244,9 @@ class _fasterRCNN(_DAFBase):
             (t_prob.detach(), t_bbox.detach(), tgt_im_info.detach(), "TEST")])
         rpn_loss_cls, rpn_loss_bbox, _ = rpn.losses(s_score, s_score_r, s_bbox, gt_boxes, im_info,
                                                     num_boxes, rng=self.replay_rng)
+        if early:
+            rpn_loss_cls, rpn_loss_bbox = early_rpn_backward(
+                rpn_loss_cls, rpn_loss_bbox, rpn_in, [(base, lambda g: g)])
         rois, tgt_rois = pending.join()
         if self.capture is not None:
             self.capture.update(s_rois=rois.detach().clone(), t_rois=tgt_rois.detach().clone())
