@@ -657,6 +657,9 @@ struct TailPlan {
 // Whole rounds of tiles over the full K, the last partial round split over K when that
 // beats running it as a mostly idle round (cost model: tile time at the slot rate, the
 // slab round trip at 4 TB/s, 6 us per reduce launch).
+#ifndef TLOD_SPLIT_BW  // slab bytes per second the split-K cost model assumes (A/B knob)
+#define TLOD_SPLIT_BW 4e12
+#endif
 TailPlan plan_tail(int T, int nchunks, int slots, double tile_s, double tile_bytes) {
   TailPlan p{T, 1, nchunks};
   double best = (double)((T + slots - 1) / slots) * tile_s;
@@ -669,7 +672,7 @@ TailPlan plan_tail(int T, int nchunks, int slots, double tile_s, double tile_byt
       if (tail <= 0) continue;
       const double t = (double)dp / slots * tile_s +
                        (double)(((long long)tail * kk + slots - 1) / slots) * tile_s * cps / nchunks +
-                       (2.0 * kk + 1.0) * tail * tile_bytes / 4e12 + 6e-6;
+                       (2.0 * kk + 1.0) * tail * tile_bytes / TLOD_SPLIT_BW + 6e-6;
       if (t < best * 0.97) {
         best = t;
         p = TailPlan{dp, kk, cps};
@@ -1087,7 +1090,11 @@ auto with_conv_gemm(int w_layout, int nprod, F&& f) {
 // efficiency 1 / 0.8 / 0.55) — the bottleneck's 1x1 convs have 64..2048 output channels on
 // maps of 38x75..150x300, so e.g. 256 -> 1024 at 38x75 takes 128-row tiles (192 tiles, not
 // 96).
+#ifndef TLOD_1X1_MI  // 0: the model below; 1 / 2 / 4 forced (A/B knob)
+#define TLOD_1X1_MI 0
+#endif
 static int conv1x1_mi(int N, int H, int W, int Cout) {
+  if (TLOD_1X1_MI) return TLOD_1X1_MI;
   const long long pt = (long long)div_up(H * W, kBN) * N;
   int best = 4;
   double best_c = 1e30;
