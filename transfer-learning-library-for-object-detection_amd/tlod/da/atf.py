@@ -30,7 +30,8 @@ from ..config import cfg
 from ..rpn.proposal import proposals_on_side_streams
 from ..detector.losses import smooth_l1_loss, weighted_loss_sum
 from ..rpn.rpn_head import _RPN
-from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, early_rpn, early_rpn_backward, image_label
+from .daf import _ImageDA, _InstanceDA, _fasterRCNN as _DAFBase, image_label
+from .daf import early_rpn, early_rpn_backward
 from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
 from ..detector.vgg16 import VGG16_SPLITS

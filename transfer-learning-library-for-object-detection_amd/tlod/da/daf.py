@@ -112,18 +112,18 @@ class _InstanceDA(nn.Module):
         return x, instance_label(x.shape[0], need_backprop)
 
 
-
 def early_rpn(model, same):
     """Early RPN backward (round 6): the RPN losses do not depend on the proposals, so their
     backward (RPN head + RPN_Conv weight / input gradients) can run on the main stream while
     the proposal layers' NMS runs on the side streams — the window in which the main stream
     otherwise waits at pending.join() with the chip nearly idle.  The RPN head then reads a
     detached copy of its input, and early_rpn_backward adds the input gradient to the
-    features' gradients by hooks in the main backward.  The returned RPN losses are detached
-    (their gradient, at weight 1 as in the reference's loss sums, methods/DAF/DAF_train.py:
-    397-400, MAF_train.py:415-418, ATF_train.py:405-408, is already in the RPN parameters' .grad): a caller that weights them differently
-    or runs a training forward without its backward sets TLOD_EARLY_RPN=0 (one backward).
-    Only on the batched (same-shape, batch 1) path."""
+    features' gradients by hooks in the main backward.  The returned RPN losses are detached:
+    their gradient, at weight 1 as in the reference's loss sums (methods/DAF/DAF_train.py:
+    397-400, MAF_train.py:415-418, ATF_train.py:405-408), is already in the RPN parameters'
+    .grad, so a caller that weights them differently or runs a training forward without its
+    backward sets TLOD_EARLY_RPN=0 (one backward).  Only on the batched (same-shape, batch 1)
+    path."""
     return (same and model.training and torch.is_grad_enabled()
             and _lib.env("TLOD_EARLY_RPN", "1") != "0")
 
@@ -141,6 +141,7 @@ def early_rpn_backward(loss_cls, loss_bbox, rpn_in, targets):
                 gs = share(g)
                 feat.register_hook(lambda gf, gs=gs: gf + gs)
     return loss_cls.detach(), loss_bbox.detach()
+
 
 class _fasterRCNN(nn.Module):
     """lib/DAF/faster_rcnn.py:22-247."""

@@ -21,7 +21,8 @@ from ..conv import Conv2d
 from ..detector.losses import weighted_loss_sum
 from ..linear import Linear
 from ..rpn.proposal import proposals_on_side_streams
-from .daf import _ImageDA, _fasterRCNN as _DAFBase, early_rpn, early_rpn_backward, grad_reverse, image_label
+from .daf import _ImageDA, _fasterRCNN as _DAFBase, grad_reverse, image_label
+from .daf import early_rpn, early_rpn_backward
 from .daf import resnet as _daf_resnet
 from .daf import vgg16 as _daf_vgg16
 from ..detector.vgg16 import VGG16_SPLITS
