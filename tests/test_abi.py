@@ -55,3 +55,28 @@ def test_product_path_refuses_cpu_tensors():
         nms(d, 0.7)
     with pytest.raises(NotImplementedError):
         nms(d, 0.7, force_cpu=True)
+
+
+def test_nhwc3_gemm_argument_checks_host_only():
+    """tlod_gemm_nhwc3_bs_f32 (round 6) rejects a bad mode, channel counts whose chunks /
+    column tiles would straddle taps, an epilogue on the weight gradient and an aliased
+    residual — before any device work (no GPU here)."""
+    import ctypes
+    from tlod import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.cast(buf, ctypes.c_void_p).value
+    q = p + 16
+
+    def call(mode, C, O, residual=None, bias=None, relu=0, c=None):
+        return L.tlod_gemm_nhwc3_bs_f32(mode, p, p, bias, residual, None, relu,
+                                        q if c is None else c, 2, 4, 4, C, O, 6, None, 0, None)
+    assert call(3, 512, 512) != 0
+    assert b"mode" in L.tlod_last_error()
+    assert call(0, 24, 512) != 0        # forward: C % 16
+    assert call(1, 512, 40) != 0        # input gradient: O % 16
+    assert call(2, 128, 512) != 0       # weight gradient: C % 256
+    assert call(2, 512, 512, bias=p) != 0
+    assert b"epilogue" in L.tlod_last_error()
+    assert call(0, 512, 512, residual=q) != 0
+    assert b"alias" in L.tlod_last_error()
