@@ -34,6 +34,8 @@ if "--atf" in sys.argv:  # the ATF-R101 RoI head (config 5): 4512 RoIs x 16 bins
     R = int(os.environ.get("ATF_ROWS", 4512 * 16))
     LAYERS = [("l4b0_conv1", 1024, 512), ("l4_conv1", 2048, 512), ("l4_conv2", 4608, 512),
               ("l4_conv3", 512, 2048), ("l4_ds", 1024, 2048)]
+if "--da" in sys.argv:  # the DAF instance-DA head (lib/DAF/DA.py:53-73) on the 556 RoIs
+    LAYERS = [("ins_fc1", 4096, 1024), ("ins_fc2", 1024, 1024)]
 NOTORCH = "--no-torch" in sys.argv
 for name, I, O in LAYERS:
     x = torch.randn(R, I, device="cuda")

@@ -726,12 +726,18 @@ struct Gemm {
   }
 };
 
+#ifndef TLOD_GEMM_SMALL_MI  // A/B knob: 64- / 128-row tiles (1 / 2) for GEMMs of < 64 tiles
+#define TLOD_GEMM_SMALL_MI 0
+#endif
 template <typename F>
-auto with_gemm(int M, int ak, int bk, int nprod, F&& f) {
+auto with_gemm(int M, int ak, int bk, int nprod, F&& f, int N = 0) {
   // M tile 192 when it pads M less (the 556 RoI rows of the head: 576 vs 768)
   const bool m192 = div_up(M, 192) * 192 < div_up(M, 256) * 256;
+  const bool small = TLOD_GEMM_SMALL_MI && N > 0 && nprod == 6 &&
+                     div_up(M, m192 ? 192 : 256) * div_up(N, kBN) < 64;
 #define TLOD_GEMM_CASE(A_, B_)                                                 \
   if (ak == A_ && bk == B_) {                                                  \
+    if (small) return f(Gemm<A_, B_, 6, TLOD_GEMM_SMALL_MI ? TLOD_GEMM_SMALL_MI : 3>{}); \
     if (m192) return nprod == 6 ? f(Gemm<A_, B_, 6, 3>{}) : f(Gemm<A_, B_, 3, 3>{}); \
     return nprod == 6 ? f(Gemm<A_, B_, 6, 4>{}) : f(Gemm<A_, B_, 3, 4>{});     \
   }
@@ -740,6 +746,7 @@ auto with_gemm(int M, int ak, int bk, int nprod, F&& f) {
   TLOD_GEMM_CASE(0, 0)
 #undef TLOD_GEMM_CASE
   // (0, 1): the callers pass 0/1 flags, so the four cases are exhaustive
+  if (small) return f(Gemm<0, 1, 6, TLOD_GEMM_SMALL_MI ? TLOD_GEMM_SMALL_MI : 3>{});
   if (m192) return nprod == 6 ? f(Gemm<0, 1, 6, 3>{}) : f(Gemm<0, 1, 3, 3>{});
   return nprod == 6 ? f(Gemm<0, 1, 6, 4>{}) : f(Gemm<0, 1, 3, 4>{});
 }
@@ -1134,7 +1141,7 @@ extern "C" size_t tlod_gemm_bs_workspace_bytes(int M, int N, int K, int a_kconti
                                                int nprod) {
   if (M <= 0 || N <= 0 || K <= 0 || (nprod != 3 && nprod != 6)) return 0;
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod,
-                   [&](auto g) { return g.ws_bytes(M, N, K); });
+                   [&](auto g) { return g.ws_bytes(M, N, K); }, N);
 }
 
 extern "C" int tlod_gemm_bs_f32(const float* a, const float* b, const float* bias, float* c, int M,
@@ -1146,7 +1153,7 @@ extern "C" int tlod_gemm_bs_f32(const float* a, const float* b, const float* bia
   TLOD_CHECK_ARG((size_t)std::max(M, N) * K * 4 < (1ull << 31), "operand too large");
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
     return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
-  });
+  }, N);
 }
 
 extern "C" int tlod_gemm_bs_ex_f32(const float* a, const float* b, const float* bias,
@@ -1160,7 +1167,7 @@ extern "C" int tlod_gemm_bs_ex_f32(const float* a, const float* b, const float* 
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
     return g.run(a, b, bias, c, M, N, K, static_cast<float*>(ws), ws_bytes, (hipStream_t)stream,
                  residual, relu);
-  });
+  }, N);
 }
 
 extern "C" int tlod_gemm_bs_mask_f32(const float* a, const float* b, const float* residual,
@@ -1174,7 +1181,7 @@ extern "C" int tlod_gemm_bs_mask_f32(const float* a, const float* b, const float
   return with_gemm(M, a_kcontig ? 1 : 0, b_kcontig ? 1 : 0, nprod, [&](auto g) {
     return g.run(a, b, nullptr, c, M, N, K, static_cast<float*>(ws), ws_bytes,
                  (hipStream_t)stream, residual, 0, mask);
-  });
+  }, N);
 }
 
 extern "C" size_t tlod_conv3x3_gemm_bs_workspace_bytes(int N, int Cin, int H, int W, int Cout,
